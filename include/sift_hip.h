@@ -1,0 +1,190 @@
+/*
+ * sift_hip.h — C-ABI boundary of the MI355X-native SIFT extractor.
+ *
+ * This is the thin shim that sits directly under the reference's public
+ * entry point
+ *     std::vector<Keypoint> detect_keypoints_and_descriptors(const Image&, ...)
+ * (reference src/sift.hh:65-71, implemented at src/sift.cpp:712-776).
+ * The C++ drop-in (sift.hh / libsift_amd.so) wraps these calls and rethrows
+ * failures as std::runtime_error, the reference's error convention
+ * (src/image.cpp:43,159,222, src/image_io.cpp:24,149).
+ *
+ * Plain pointers and sizes only: no torch, no C++ types, no HIP types in the
+ * signatures (streams are passed as opaque void*).
+ *
+ * All status codes: 0 = success, negative = error (see sift_hip_strerror).
+ */
+#ifndef SIFT_HIP_H
+#define SIFT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIFT_HIP_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define SIFT_OK 0
+#define SIFT_ERR_ARG -1          /* bad argument (null pointer, bad size)     */
+#define SIFT_ERR_CHANNELS -2     /* channels not in {1,3}: reference reads
+                                    past the pixel for c=2 (image.cpp:16-18)  */
+#define SIFT_ERR_TOO_SMALL -3    /* min(W0,H0)/3 == 0: the reference takes
+                                    log2(0) (sift.cpp:134), undefined         */
+#define SIFT_ERR_HIP -4          /* a HIP runtime call failed                  */
+#define SIFT_ERR_NOMEM -5        /* device or host allocation failed           */
+#define SIFT_ERR_NO_DEVICE -6    /* no HIP device / bad device index           */
+#define SIFT_ERR_PARAM -7        /* parameter outside the supported range      */
+#define SIFT_ERR_STATE -8        /* call order violated (e.g. no prior detect) */
+
+/*
+ * Parameters of detect_keypoints_and_descriptors (reference sift.hh:65-71),
+ * same names, same defaults (see sift_params_default), plus two extensions:
+ *   max_octaves        0 = the reference formula floor(log2(min(W0,H0)/3))
+ *                      (sift.cpp:132-137); >0 caps the octave count
+ *                      (needed for BASELINE config 3, "5 octaves").
+ *   write_keypoints_png reserved for the reference's keypoints.png side effect
+ *                      (sift.cpp:765-768); the C-ABI never writes files, the
+ *                      C++ drop-in honours it.
+ * num_bins is a double in the reference API and is narrowed to int by
+ * compute_orientations (sift.cpp:450); it is narrowed the same way here.
+ */
+typedef struct sift_params {
+    int double_image_size;      /* true  */
+    int intervals;              /* 3     */
+    int window_size;            /* 3     */
+    int max_octaves;            /* 0 (extension) */
+    double init_sigma;          /* 1.6   */
+    double contrast_threshold;  /* 0.04  */
+    double eigen_ratio;         /* 10.0  */
+    double num_bins;            /* 36    */
+    double peak_ratio;          /* 0.8   */
+    double ori_sigma_factor;    /* 1.5   */
+    double desc_scale_factor;   /* 3.0   */
+    int write_keypoints_png;    /* 0 in the C-ABI (extension) */
+    int reserved;
+} sift_params;
+
+/*
+ * One keypoint record. Layout-identical to the reference struct Keypoint
+ * (sift.hh:15-23): x@0 y@8 octave@16 layer@20 size@24 pori@32 desc@40,
+ * sizeof == 168, so a sift_kp array can be memcpy'd into
+ * std::vector<Keypoint> storage.
+ */
+typedef struct sift_kp {
+    double x;
+    double y;
+    int octave;
+    int layer;
+    double size;
+    double pori;
+    uint8_t desc[128];
+} sift_kp;
+
+/* Candidate extremum (x, y, DoG layer z, octave) — reference tuple
+ * Extrema (sift.cpp:14), with x,y stored as ints (they are integral). */
+typedef struct sift_extremum {
+    int x;
+    int y;
+    int z;
+    int octave;
+} sift_extremum;
+
+typedef struct sift_ctx sift_ctx;
+
+/* Fill *p with the reference defaults (sift.hh:65-71). */
+void sift_params_default(sift_params* p);
+
+/* Create a context bound to HIP device `device`: owns one HIP stream and a
+ * device arena that grows to the largest image seen. */
+int sift_hip_create(int device, sift_ctx** out);
+int sift_hip_destroy(sift_ctx* ctx);
+
+/*
+ * Full pipeline on one image (reference sift.cpp:712-776 minus the PNG side
+ * effect). `hwc` is the reference Image buffer: interleaved HWC doubles,
+ * data[(y*w+x)*c+ch] (image_io.cpp:81-92), host memory.
+ * On success *out_kps (n records, sorted and de-duplicated exactly as
+ * clean_keypoints, sift.cpp:20-24) is allocated by the library; release it
+ * with sift_hip_free. If out_desc_f32 is non-null it receives n*128 floats:
+ * the normalised descriptor h*norm_inv of convert_hist_to_desc
+ * (sift.cpp:599-601) before the x512 quantisation (for the 1e-4 check).
+ */
+int sift_hip_detect(sift_ctx* ctx, const double* hwc, int w, int h, int c,
+                    const sift_params* p, sift_kp** out_kps, size_t* out_n,
+                    float** out_desc_f32);
+
+/* Same, but `d_hwc` is a device pointer on the context's device (input
+ * already resident in HBM). */
+int sift_hip_detect_device(sift_ctx* ctx, const double* d_hwc, int w, int h,
+                           int c, const sift_params* p, sift_kp** out_kps,
+                           size_t* out_n, float** out_desc_f32);
+
+void sift_hip_free(void* p);
+const char* sift_hip_strerror(int status);
+
+/* ---- introspection of the last detect (tests, bench, multi-GPU) -------- */
+
+/* Pipeline counts of the last detect: extrema candidates, refined
+ * keypoints, oriented keypoints (pre-dedup), final keypoints, octaves. */
+typedef struct sift_counts {
+    int64_t extrema;
+    int64_t refined;
+    int64_t oriented;
+    int64_t final_n;
+    int octaves;
+    int levels_per_octave;
+    int octave0_w;
+    int octave0_h;
+} sift_counts;
+int sift_hip_last_counts(sift_ctx* ctx, sift_counts* out);
+
+/* Copy Gaussian level G[octave][level] of the last detect to host
+ * (w_o*h_o doubles, row-major). Level 0 of octave o>0 is the decimated base. */
+int sift_hip_copy_level(sift_ctx* ctx, int octave, int level, double* host_out,
+                        size_t cap_elems, int* w_out, int* h_out);
+
+/* Copy the extrema candidate list of the last detect (unordered). */
+int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out,
+                          size_t cap, size_t* n_out);
+
+/* Device-side pre-dedup keypoint records of the last detect (n records of
+ * sift_kp, unordered): copied device-to-device into `d_dst` (a buffer on the
+ * same device) on the context stream, then synchronised. Used by the
+ * multi-GPU driver for the RCCL all-gather of descriptor buffers. */
+int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap,
+                                 size_t* n_out);
+
+/* The context's HIP stream (hipStream_t), for event timing. */
+void* sift_hip_stream(sift_ctx* ctx);
+
+/*
+ * Per-kernel timing of the pyramid (blur) kernels with HIP events on the
+ * context stream. When enabled, every blur launch is bracketed by events;
+ * sift_hip_blur_profile returns the accumulated kernel time (ms), the
+ * number of launches and their algorithmic HBM bytes (read src once, write
+ * dst once: 16 B/px, plus 8 B per decimated px) since the last reset.
+ */
+int sift_hip_set_profiling(sift_ctx* ctx, int enable);
+int sift_hip_blur_profile(sift_ctx* ctx, double* ms, int64_t* launches,
+                          double* bytes, int reset);
+
+/* ---- synthetic input (bench + tests) ----------------------------------- */
+/*
+ * Deterministic synthetic gray image, bit-reproducible on any IEEE-754
+ * machine (integer RNG + basic-op polynomials, no libm): background
+ * 128+40*sin(x/37)*cos(y/53) plus `nblobs` Gaussian blobs with
+ * sigma in [1.5, 1.5+smax] and amplitude in [-100,100], clamped to [0,255]
+ * and rounded to integers (SURVEY §6 workload class, portable generator).
+ * out: w*h doubles. channels==3 replicates a tinted RGB version.
+ */
+int sift_synth_image(int w, int h, int channels, int64_t nblobs, double smax,
+                     uint64_t seed, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SIFT_HIP_H */

@@ -1,0 +1,607 @@
+// sift_ctx.hip — C-ABI boundary (include/sift_hip.h) and host orchestration
+// of the MI355X SIFT pipeline.
+//
+// Replaces the body of detect_keypoints_and_descriptors (reference
+// src/sift.cpp:712-776). Host work is limited to what the reference computes
+// with glibc and that feeds bit-exact outputs: the octave count
+// (sift.cpp:132-137), the level sigmas (sift.cpp:143-155), the blur taps
+// (image.cpp:226-235), the final keypoint size (std::pow, sift.cpp:427-429)
+// and clean_keypoints (std::sort + std::unique, sift.cpp:20-24). Everything
+// per-pixel and per-keypoint runs in the HIP kernels of sift_kernels.hip,
+// enqueued on one stream with no host synchronisation until the counters are
+// read back at the end.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <numeric>
+#include <vector>
+
+#include "sift_kernels.h"
+
+using namespace sift_amd;
+
+namespace {
+
+struct EventPair {
+    hipEvent_t a, b;
+    double bytes;
+};
+
+}  // namespace
+
+struct sift_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+
+    double* d_in = nullptr;
+    size_t in_cap = 0;  // elements
+    double* d_pyr = nullptr;
+    size_t pyr_cap = 0;
+    double* d_tmp = nullptr;
+    size_t tmp_cap = 0;
+
+    sift_extremum* d_cand = nullptr;
+    RawKp* d_raw = nullptr;
+    sift_kp* d_ori = nullptr;
+    double* d_off0 = nullptr;
+    float* d_df32 = nullptr;
+    unsigned cap_cand = 0, cap_raw = 0, cap_ori = 0, cap_off0 = 0, cap_df32 = 0;
+    unsigned* d_ctr = nullptr;
+    unsigned* h_ctr = nullptr;  // pinned
+    PyrTable h_pt{};
+    PyrTable* d_pt = nullptr;
+
+    // last detect
+    bool have_run = false;
+    sift_counts counts{};
+    sift_params last_p{};
+
+    // profiling
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<EventPair> pending;
+    double prof_ms = 0.0;
+    int64_t prof_launches = 0;
+    double prof_bytes = 0.0;
+
+    // host staging
+    std::vector<sift_kp> h_ori;
+    std::vector<double> h_off0;
+    std::vector<float> h_df32;
+};
+
+namespace {
+
+#define SIFT_HIP_TRY(expr)                          \
+    do {                                            \
+        hipError_t e_ = (expr);                     \
+        if (e_ != hipSuccess) return SIFT_ERR_HIP;  \
+    } while (0)
+
+int ensure(double** p, size_t* cap, size_t need) {
+    if (*cap >= need) return SIFT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, need * sizeof(double)) != hipSuccess) return SIFT_ERR_NOMEM;
+    *cap = need;
+    return SIFT_OK;
+}
+
+template <class T>
+int ensure_t(T** p, unsigned* cap, unsigned need) {
+    if (*cap >= need && *p) return SIFT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, (size_t)need * sizeof(T)) != hipSuccess) return SIFT_ERR_NOMEM;
+    *cap = need;
+    return SIFT_OK;
+}
+
+// apply_gaussian_blur_fast kernel construction (image.cpp:226-235) and the
+// running sum_w of apply_double_convolution_1d (image.cpp:171-185).
+bool make_taps(double sigma, BlurTaps* t) {
+    const double ks_d = std::ceil(3 * sigma);
+    if (!(ks_d >= 0) || ks_d + 1 > kMaxTaps) return false;
+    const int ks = (int)ks_d + 1;
+    std::memset(t, 0, sizeof *t);
+    const double exp_denom = 2 * sigma * sigma;
+    const double coef = 1 / (std::sqrt(2 * M_PI) * sigma);
+    for (int i = 0; i < ks; ++i) t->k[i] = std::exp(-i * i / exp_denom) * coef;
+    double s = t->k[0];
+    for (int u = 1; u < ks; ++u) s += 2.0 * t->k[u];
+    t->sum_w = s;
+    t->R = ks - 1;
+    return true;
+}
+
+bool kp_less(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator<, sift.hh:31-41
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.pori != b.pori) return a.pori < b.pori;
+    return a.octave > b.octave;
+}
+bool kp_equal(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator==, sift.hh:25-27
+    return a.x == b.x && a.y == b.y && a.size == b.size && a.pori == b.pori;
+}
+
+hipEvent_t next_event(sift_ctx* ctx) {
+    if (ctx->ev_used == ctx->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        ctx->ev_pool.push_back(e);
+    }
+    return ctx->ev_pool[ctx->ev_used++];
+}
+
+struct Geometry {
+    int octaves = 0;
+    int n_gauss = 0;
+    int W[kMaxOctaves] = {0};
+    int H[kMaxOctaves] = {0};
+    size_t offs[kMaxOctaves][kMaxLevels] = {{0}};
+    size_t total = 0;   // doubles in the pyramid
+    size_t sum_px = 0;  // sum over octaves of W*H
+};
+
+int plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* taps_init,
+         BlurTaps* taps, DevParams* dp) {
+    if (w <= 0 || h <= 0) return SIFT_ERR_ARG;
+    if (c != 1 && c != 3) return SIFT_ERR_CHANNELS;
+    if (p->intervals < 1 || p->intervals + 3 > kMaxLevels) return SIFT_ERR_PARAM;
+    if (p->window_size < 2 || p->window_size / 2 > 3) return SIFT_ERR_PARAM;
+    const int nb = (int)p->num_bins;
+    if (nb < 1 || nb > kMaxBins) return SIFT_ERR_PARAM;
+    if (!(p->init_sigma * p->init_sigma - 1 > 0)) return SIFT_ERR_PARAM;
+    if (p->max_octaves < 0) return SIFT_ERR_PARAM;
+
+    const int W0 = p->double_image_size ? 2 * w : w;
+    const int H0 = p->double_image_size ? 2 * h : h;
+    // compute_octaves_count (sift.cpp:132-137), integer division by 3
+    const int q = std::min(W0, H0) / 3;
+    if (q == 0) return SIFT_ERR_TOO_SMALL;
+    int octaves = (int)std::floor(std::log2(q));
+    if (p->max_octaves > 0 && octaves > p->max_octaves) octaves = p->max_octaves;
+    if (octaves < 1 || octaves > kMaxOctaves) return SIFT_ERR_TOO_SMALL;
+    g->octaves = octaves;
+    g->n_gauss = p->intervals + 3;
+    int Wo = W0, Ho = H0;
+    size_t off = 0;
+    for (int o = 0; o < octaves; ++o) {
+        // the reference decimates after every octave and throws when the
+        // level is smaller than 2x2 (image.cpp:42-44, sift.cpp:195)
+        if (Wo < 2 || Ho < 2) return SIFT_ERR_TOO_SMALL;
+        g->W[o] = Wo;
+        g->H[o] = Ho;
+        g->sum_px += (size_t)Wo * Ho;
+        for (int l = 0; l < g->n_gauss; ++l) {
+            g->offs[o][l] = off;
+            off += (size_t)Wo * Ho;
+        }
+        Wo /= 2;
+        Ho /= 2;
+    }
+    g->total = off;
+
+    // compute_gaussian_kernels (sift.cpp:143-155)
+    std::vector<double> sig(g->n_gauss);
+    sig[0] = p->init_sigma;
+    const double k = std::pow(2.0, 1.0 / p->intervals);
+    for (int i = 1; i < g->n_gauss; ++i) {
+        const double prev = (std::pow(k, i - 1)) * p->init_sigma;
+        sig[i] = prev * std::sqrt(k * k - 1);
+    }
+    if (!make_taps(std::sqrt(p->init_sigma * p->init_sigma - 1), taps_init))
+        return SIFT_ERR_PARAM;
+    for (int i = 1; i < g->n_gauss; ++i)
+        if (!make_taps(sig[i], &taps[i])) return SIFT_ERR_PARAM;
+
+    dp->intervals = p->intervals;
+    dp->window_size = p->window_size;
+    dp->num_bins = nb;
+    dp->double_image = p->double_image_size ? 1 : 0;
+    // detect_extrema: double threshold passed into an int (sift.cpp:266,305-307)
+    dp->threshold = (int)std::floor(0.5 * p->contrast_threshold /
+                                    static_cast<double>(p->intervals) * 255.0);
+    dp->n_dog = p->intervals + 2;
+    dp->n_gauss = g->n_gauss;
+    dp->octaves = octaves;
+    dp->init_sigma = p->init_sigma;
+    dp->contrast_threshold = p->contrast_threshold;
+    dp->eigen_ratio = p->eigen_ratio;
+    dp->peak_ratio = p->peak_ratio;
+    dp->ori_sigma_factor = p->ori_sigma_factor;
+    dp->desc_scale_factor = p->desc_scale_factor;
+    return SIFT_OK;
+}
+
+int blur_launch(sift_ctx* ctx, const double* src, double* dst, int W, int H,
+                const BlurTaps& t, double* dec, int Wd, int Hd) {
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (ctx->profiling) {
+        ea = next_event(ctx);
+        eb = next_event(ctx);
+        if (!ea || !eb) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(hipEventRecord(ea, ctx->stream));
+    }
+    if (t.R > kMaxTemplR || t.R < 1) {
+        if (ensure(&ctx->d_tmp, &ctx->tmp_cap, (size_t)W * H) != SIFT_OK) return SIFT_ERR_NOMEM;
+    }
+    SIFT_HIP_TRY(launch_blur(src, dst, W, H, t, dec, Wd, Hd, ctx->d_tmp, ctx->stream));
+    if (ctx->profiling) {
+        SIFT_HIP_TRY(hipEventRecord(eb, ctx->stream));
+        double bytes = 16.0 * (double)W * (double)H;
+        if (dec) bytes += 8.0 * (double)Wd * (double)Hd;
+        ctx->pending.push_back({ea, eb, bytes});
+    }
+    return SIFT_OK;
+}
+
+int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
+                const sift_params* p, sift_kp** out_kps, size_t* out_n,
+                float** out_desc_f32) {
+    Geometry g;
+    BlurTaps taps_init;
+    std::vector<BlurTaps> taps(kMaxLevels);
+    DevParams dp;
+    int st = plan(p, w, h, c, &g, &taps_init, taps.data(), &dp);
+    if (st != SIFT_OK) return st;
+    SIFT_HIP_TRY(hipSetDevice(ctx->device));
+    ctx->have_run = false;
+    ctx->ev_used = 0;
+    ctx->pending.clear();
+
+    if ((st = ensure(&ctx->d_pyr, &ctx->pyr_cap, g.total)) != SIFT_OK) return st;
+    std::memset(&ctx->h_pt, 0, sizeof ctx->h_pt);
+    for (int o = 0; o < g.octaves; ++o) {
+        ctx->h_pt.w[o] = g.W[o];
+        ctx->h_pt.h[o] = g.H[o];
+        for (int l = 0; l < g.n_gauss; ++l) ctx->h_pt.lvl[o][l] = ctx->d_pyr + g.offs[o][l];
+    }
+    SIFT_HIP_TRY(hipMemcpyAsync(ctx->d_pt, &ctx->h_pt, sizeof(PyrTable),
+                                hipMemcpyHostToDevice, ctx->stream));
+
+    // capacities for the variable-size stages; grown and re-run on overflow
+    unsigned want_cand = (unsigned)std::min<size_t>(std::max<size_t>(g.sum_px / 32, 65536),
+                                                   (size_t)1 << 28);
+    if ((st = ensure_t(&ctx->d_cand, &ctx->cap_cand, want_cand)) != SIFT_OK) return st;
+    if ((st = ensure_t(&ctx->d_raw, &ctx->cap_raw, ctx->cap_cand)) != SIFT_OK) return st;
+    if ((st = ensure_t(&ctx->d_ori, &ctx->cap_ori, 2 * ctx->cap_raw)) != SIFT_OK) return st;
+    if ((st = ensure_t(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
+    if (out_desc_f32 &&
+        (st = ensure_t(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
+        return st;
+
+    // ---- Gaussian pyramid (compute_initial_image + compute_gaussian_images)
+    const int W0 = g.W[0], H0 = g.H[0];
+    double* G00 = ctx->h_pt.lvl[0][0];
+    const double* base_src = d_img;
+    if (c != 1 || p->double_image_size) {
+        // gray (+ bilinear x2) into level 1's storage; level 1 is written by
+        // the first octave blur, after G[0][0] has been produced from it
+        double* scratch = ctx->h_pt.lvl[0][1];
+        SIFT_HIP_TRY(launch_prepare(d_img, w, h, c, p->double_image_size ? 1 : 0, scratch,
+                                    W0, H0, ctx->stream));
+        base_src = scratch;
+    }
+    if ((st = blur_launch(ctx, base_src, G00, W0, H0, taps_init, nullptr, 0, 0)) != SIFT_OK)
+        return st;
+    const int dec_level = g.n_gauss - 3;  // = intervals (sift.cpp:195-196)
+    for (int o = 0; o < g.octaves; ++o) {
+        for (int l = 1; l < g.n_gauss; ++l) {
+            const bool dec = (l == dec_level) && (o + 1 < g.octaves);
+            st = blur_launch(ctx, ctx->h_pt.lvl[o][l - 1], ctx->h_pt.lvl[o][l], g.W[o], g.H[o],
+                             taps[l], dec ? ctx->h_pt.lvl[o + 1][0] : nullptr,
+                             dec ? g.W[o + 1] : 0, dec ? g.H[o + 1] : 0);
+            if (st != SIFT_OK) return st;
+        }
+    }
+
+    // ---- extrema -> refine -> orientation -> descriptor, re-run on overflow
+    for (int attempt = 0;; ++attempt) {
+        SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, 4 * sizeof(unsigned), ctx->stream));
+        for (int o = 0; o < g.octaves; ++o)
+            SIFT_HIP_TRY(launch_extrema(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
+                                        p->window_size, dp.threshold, ctx->d_cand,
+                                        ctx->d_ctr + 0, ctx->cap_cand, ctx->stream));
+        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, ctx->d_ctr + 0, ctx->cap_cand,
+                                   ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, ctx->stream));
+        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw,
+                                   ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2, ctx->cap_ori,
+                                   ctx->stream));
+        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, ctx->d_ctr + 2, ctx->cap_ori,
+                                       out_desc_f32 ? ctx->d_df32 : nullptr, ctx->stream));
+        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+        const unsigned nc = ctx->h_ctr[0], nr = ctx->h_ctr[1], no = ctx->h_ctr[2];
+        if (nc <= ctx->cap_cand && nr <= ctx->cap_raw && no <= ctx->cap_ori) break;
+        if (attempt >= 3) return SIFT_ERR_NOMEM;
+        // grow every stage that overflowed (refine/orient counts are lower
+        // bounds when an upstream stage overflowed, so grow generously)
+        const unsigned nc2 = std::max(ctx->cap_cand, nc) * 2u;
+        const unsigned nr2 = std::max(std::max(ctx->cap_raw, nr) * 2u, nc2);
+        const unsigned no2 = std::max(std::max(ctx->cap_ori, no) * 2u, 2u * nr2);
+        if ((st = ensure_t(&ctx->d_cand, &ctx->cap_cand, nc2)) != SIFT_OK) return st;
+        if ((st = ensure_t(&ctx->d_raw, &ctx->cap_raw, nr2)) != SIFT_OK) return st;
+        if ((st = ensure_t(&ctx->d_ori, &ctx->cap_ori, no2)) != SIFT_OK) return st;
+        if ((st = ensure_t(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
+        if (out_desc_f32 &&
+            (st = ensure_t(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
+            return st;
+    }
+
+    const unsigned n_ori = ctx->h_ctr[2];
+    ctx->h_ori.resize(n_ori);
+    ctx->h_off0.resize(n_ori);
+    if (n_ori) {
+        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.data(), ctx->d_ori, n_ori * sizeof(sift_kp),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.data(), ctx->d_off0, n_ori * sizeof(double),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (out_desc_f32) {
+        ctx->h_df32.resize((size_t)n_ori * 128);
+        if (n_ori)
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.data(), ctx->d_df32,
+                                        (size_t)n_ori * 128 * sizeof(float),
+                                        hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+
+    if (ctx->profiling) {
+        for (const EventPair& e : ctx->pending) {
+            float ms = 0.f;
+            SIFT_HIP_TRY(hipEventElapsedTime(&ms, e.a, e.b));
+            ctx->prof_ms += ms;
+            ctx->prof_bytes += e.bytes;
+            ctx->prof_launches += 1;
+        }
+        ctx->pending.clear();
+    }
+
+    // final size with glibc pow (sift.cpp:427-429, halved at sift.cpp:525)
+    for (unsigned i = 0; i < n_ori; ++i) {
+        sift_kp& r = ctx->h_ori[i];
+        const double scale = std::pow(2, r.octave);
+        double size = p->init_sigma * scale *
+                      std::pow(2, (static_cast<double>(r.layer) + ctx->h_off0[i]) / p->intervals);
+        if (p->double_image_size) size /= 2;
+        r.size = size;
+    }
+    // clean_keypoints (sift.cpp:20-24): sort then unique on (x, y, size, pori)
+    std::vector<unsigned> idx(n_ori);
+    std::iota(idx.begin(), idx.end(), 0u);
+    std::sort(idx.begin(), idx.end(), [&](unsigned a, unsigned b) {
+        return kp_less(ctx->h_ori[a], ctx->h_ori[b]);
+    });
+    std::vector<unsigned> keep;
+    keep.reserve(n_ori);
+    for (unsigned i = 0; i < n_ori; ++i)
+        if (keep.empty() || !kp_equal(ctx->h_ori[keep.back()], ctx->h_ori[idx[i]]))
+            keep.push_back(idx[i]);
+
+    const size_t n = keep.size();
+    sift_kp* kps = (sift_kp*)std::malloc(std::max<size_t>(n, 1) * sizeof(sift_kp));
+    if (!kps) return SIFT_ERR_NOMEM;
+    for (size_t i = 0; i < n; ++i) kps[i] = ctx->h_ori[keep[i]];
+    float* df = nullptr;
+    if (out_desc_f32) {
+        df = (float*)std::malloc(std::max<size_t>(n, 1) * 128 * sizeof(float));
+        if (!df) {
+            std::free(kps);
+            return SIFT_ERR_NOMEM;
+        }
+        for (size_t i = 0; i < n; ++i)
+            std::memcpy(df + i * 128, ctx->h_df32.data() + (size_t)keep[i] * 128,
+                        128 * sizeof(float));
+    }
+    *out_kps = kps;
+    *out_n = n;
+    if (out_desc_f32) *out_desc_f32 = df;
+
+    ctx->counts.extrema = ctx->h_ctr[0];
+    ctx->counts.refined = ctx->h_ctr[1];
+    ctx->counts.oriented = n_ori;
+    ctx->counts.final_n = (int64_t)n;
+    ctx->counts.octaves = g.octaves;
+    ctx->counts.levels_per_octave = g.n_gauss;
+    ctx->counts.octave0_w = g.W[0];
+    ctx->counts.octave0_h = g.H[0];
+    ctx->last_p = *p;
+    ctx->have_run = true;
+    return SIFT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void sift_params_default(sift_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof *p);
+    p->double_image_size = 1;
+    p->intervals = 3;
+    p->window_size = 3;
+    p->max_octaves = 0;
+    p->init_sigma = 1.6;
+    p->contrast_threshold = 0.04;
+    p->eigen_ratio = 10.0;
+    p->num_bins = 36;
+    p->peak_ratio = 0.8;
+    p->ori_sigma_factor = 1.5;
+    p->desc_scale_factor = 3.0;
+    p->write_keypoints_png = 0;
+}
+
+int sift_hip_create(int device, sift_ctx** out) {
+    if (!out) return SIFT_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SIFT_ERR_NO_DEVICE;
+    if (device < 0 || device >= ndev) return SIFT_ERR_NO_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return SIFT_ERR_HIP;
+    sift_ctx* ctx = new (std::nothrow) sift_ctx();
+    if (!ctx) return SIFT_ERR_NOMEM;
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&ctx->d_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
+        hipMalloc(&ctx->d_pt, sizeof(PyrTable)) != hipSuccess) {
+        sift_hip_destroy(ctx);
+        return SIFT_ERR_HIP;
+    }
+    *out = ctx;
+    return SIFT_OK;
+}
+
+int sift_hip_destroy(sift_ctx* ctx) {
+    if (!ctx) return SIFT_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    void* bufs[] = {ctx->d_in, ctx->d_pyr, ctx->d_tmp, ctx->d_cand, ctx->d_raw,
+                    ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_pt};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (ctx->h_ctr) (void)hipHostFree(ctx->h_ctr);
+    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SIFT_OK;
+}
+
+int sift_hip_detect(sift_ctx* ctx, const double* hwc, int w, int h, int c,
+                    const sift_params* p, sift_kp** out_kps, size_t* out_n,
+                    float** out_desc_f32) {
+    if (!ctx || !hwc || !out_kps || !out_n) return SIFT_ERR_ARG;
+    if (w <= 0 || h <= 0) return SIFT_ERR_ARG;
+    if (c != 1 && c != 3) return SIFT_ERR_CHANNELS;
+    sift_params def;
+    if (!p) {
+        sift_params_default(&def);
+        p = &def;
+    }
+    SIFT_HIP_TRY(hipSetDevice(ctx->device));
+    const size_t ne = (size_t)w * h * c;
+    int st = ensure(&ctx->d_in, &ctx->in_cap, ne);
+    if (st != SIFT_OK) return st;
+    SIFT_HIP_TRY(hipMemcpyAsync(ctx->d_in, hwc, ne * sizeof(double), hipMemcpyHostToDevice,
+                                ctx->stream));
+    return detect_impl(ctx, ctx->d_in, w, h, c, p, out_kps, out_n, out_desc_f32);
+}
+
+int sift_hip_detect_device(sift_ctx* ctx, const double* d_hwc, int w, int h, int c,
+                           const sift_params* p, sift_kp** out_kps, size_t* out_n,
+                           float** out_desc_f32) {
+    if (!ctx || !d_hwc || !out_kps || !out_n) return SIFT_ERR_ARG;
+    sift_params def;
+    if (!p) {
+        sift_params_default(&def);
+        p = &def;
+    }
+    return detect_impl(ctx, d_hwc, w, h, c, p, out_kps, out_n, out_desc_f32);
+}
+
+void sift_hip_free(void* p) { std::free(p); }
+
+const char* sift_hip_strerror(int status) {
+    switch (status) {
+        case SIFT_OK: return "ok";
+        case SIFT_ERR_ARG: return "invalid argument";
+        case SIFT_ERR_CHANNELS: return "unsupported channel count (1 or 3)";
+        case SIFT_ERR_TOO_SMALL: return "image too small for the octave pyramid";
+        case SIFT_ERR_HIP: return "HIP runtime error";
+        case SIFT_ERR_NOMEM: return "out of memory";
+        case SIFT_ERR_NO_DEVICE: return "no such HIP device";
+        case SIFT_ERR_PARAM: return "parameter outside the supported range";
+        case SIFT_ERR_STATE: return "no previous detect on this context";
+        default: return "unknown error";
+    }
+}
+
+int sift_hip_last_counts(sift_ctx* ctx, sift_counts* out) {
+    if (!ctx || !out) return SIFT_ERR_ARG;
+    if (!ctx->have_run) return SIFT_ERR_STATE;
+    *out = ctx->counts;
+    return SIFT_OK;
+}
+
+int sift_hip_copy_level(sift_ctx* ctx, int octave, int level, double* host_out,
+                        size_t cap_elems, int* w_out, int* h_out) {
+    if (!ctx || !host_out) return SIFT_ERR_ARG;
+    if (!ctx->have_run) return SIFT_ERR_STATE;
+    if (octave < 0 || octave >= ctx->counts.octaves || level < 0 ||
+        level >= ctx->counts.levels_per_octave)
+        return SIFT_ERR_ARG;
+    const int W = ctx->h_pt.w[octave], H = ctx->h_pt.h[octave];
+    if (cap_elems < (size_t)W * H) return SIFT_ERR_ARG;
+    SIFT_HIP_TRY(hipSetDevice(ctx->device));
+    SIFT_HIP_TRY(hipMemcpyAsync(host_out, ctx->h_pt.lvl[octave][level],
+                                (size_t)W * H * sizeof(double), hipMemcpyDeviceToHost,
+                                ctx->stream));
+    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (w_out) *w_out = W;
+    if (h_out) *h_out = H;
+    return SIFT_OK;
+}
+
+int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out, size_t cap, size_t* n_out) {
+    if (!ctx || !n_out) return SIFT_ERR_ARG;
+    if (!ctx->have_run) return SIFT_ERR_STATE;
+    const size_t n = (size_t)ctx->counts.extrema;
+    *n_out = n;
+    if (!host_out) return SIFT_OK;
+    if (cap < n) return SIFT_ERR_ARG;
+    SIFT_HIP_TRY(hipSetDevice(ctx->device));
+    if (n)
+        SIFT_HIP_TRY(hipMemcpyAsync(host_out, ctx->d_cand, n * sizeof(sift_extremum),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SIFT_OK;
+}
+
+int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t* n_out) {
+    if (!ctx || !n_out) return SIFT_ERR_ARG;
+    if (!ctx->have_run) return SIFT_ERR_STATE;
+    const size_t n = (size_t)ctx->counts.oriented;
+    *n_out = n;
+    if (!d_dst) return SIFT_OK;
+    if (cap < n) return SIFT_ERR_ARG;
+    SIFT_HIP_TRY(hipSetDevice(ctx->device));
+    if (n)
+        SIFT_HIP_TRY(hipMemcpyAsync(d_dst, ctx->d_ori, n * sizeof(sift_kp),
+                                    hipMemcpyDeviceToDevice, ctx->stream));
+    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SIFT_OK;
+}
+
+void* sift_hip_stream(sift_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int sift_hip_set_profiling(sift_ctx* ctx, int enable) {
+    if (!ctx) return SIFT_ERR_ARG;
+    ctx->profiling = enable != 0;
+    return SIFT_OK;
+}
+
+int sift_hip_blur_profile(sift_ctx* ctx, double* ms, int64_t* launches, double* bytes,
+                          int reset) {
+    if (!ctx) return SIFT_ERR_ARG;
+    if (ms) *ms = ctx->prof_ms;
+    if (launches) *launches = ctx->prof_launches;
+    if (bytes) *bytes = ctx->prof_bytes;
+    if (reset) {
+        ctx->prof_ms = 0.0;
+        ctx->prof_launches = 0;
+        ctx->prof_bytes = 0.0;
+    }
+    return SIFT_OK;
+}
+
+}  // extern "C"

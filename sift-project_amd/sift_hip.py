@@ -1,0 +1,319 @@
+"""ctypes binding of the MI355X SIFT C-ABI (include/sift_hip.h).
+
+Python-side mirror of the reference entry point
+``detect_keypoints_and_descriptors`` (reference src/sift.hh:65-71,
+src/sift.cpp:712-776): same parameter names and defaults, keypoints returned
+as a numpy structured array whose dtype is byte-identical to the reference
+``struct Keypoint`` (168 B, sift.hh:15-23). Errors raise ``RuntimeError``,
+the reference's ``std::runtime_error`` convention.
+
+This module loads ``libsift_hip.so`` from this directory and fails loudly if
+it is missing: there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, fields
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsift_hip.so")
+
+KP_DTYPE = np.dtype(
+    [
+        ("x", "<f8"),
+        ("y", "<f8"),
+        ("octave", "<i4"),
+        ("layer", "<i4"),
+        ("size", "<f8"),
+        ("pori", "<f8"),
+        ("desc", "u1", (128,)),
+    ]
+)
+assert KP_DTYPE.itemsize == 168
+
+EXT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("z", "<i4"), ("octave", "<i4")])
+
+ERRORS = {
+    0: "ok",
+    -1: "invalid argument",
+    -2: "unsupported channel count (1 or 3)",
+    -3: "image too small for the octave pyramid",
+    -4: "HIP runtime error",
+    -5: "out of memory",
+    -6: "no such HIP device",
+    -7: "parameter outside the supported range",
+    -8: "no previous detect on this context",
+}
+
+# exported symbols declared in include/sift_hip.h
+EXPORTS = (
+    "sift_params_default",
+    "sift_hip_create",
+    "sift_hip_destroy",
+    "sift_hip_detect",
+    "sift_hip_detect_device",
+    "sift_hip_free",
+    "sift_hip_strerror",
+    "sift_hip_last_counts",
+    "sift_hip_copy_level",
+    "sift_hip_copy_extrema",
+    "sift_hip_copy_records_device",
+    "sift_hip_stream",
+    "sift_hip_set_profiling",
+    "sift_hip_blur_profile",
+    "sift_synth_image",
+)
+
+
+class CParams(ctypes.Structure):
+    _fields_ = [
+        ("double_image_size", ctypes.c_int),
+        ("intervals", ctypes.c_int),
+        ("window_size", ctypes.c_int),
+        ("max_octaves", ctypes.c_int),
+        ("init_sigma", ctypes.c_double),
+        ("contrast_threshold", ctypes.c_double),
+        ("eigen_ratio", ctypes.c_double),
+        ("num_bins", ctypes.c_double),
+        ("peak_ratio", ctypes.c_double),
+        ("ori_sigma_factor", ctypes.c_double),
+        ("desc_scale_factor", ctypes.c_double),
+        ("write_keypoints_png", ctypes.c_int),
+        ("reserved", ctypes.c_int),
+    ]
+
+
+class CCounts(ctypes.Structure):
+    _fields_ = [
+        ("extrema", ctypes.c_int64),
+        ("refined", ctypes.c_int64),
+        ("oriented", ctypes.c_int64),
+        ("final_n", ctypes.c_int64),
+        ("octaves", ctypes.c_int),
+        ("levels_per_octave", ctypes.c_int),
+        ("octave0_w", ctypes.c_int),
+        ("octave0_h", ctypes.c_int),
+    ]
+
+
+@dataclass
+class SiftParams:
+    """detect_keypoints_and_descriptors parameters (reference sift.hh:65-71)."""
+
+    double_image_size: bool = True
+    init_sigma: float = 1.6
+    intervals: int = 3
+    window_size: int = 3
+    contrast_threshold: float = 0.04
+    eigen_ratio: float = 10.0
+    num_bins: float = 36
+    peak_ratio: float = 0.8
+    ori_sigma_factor: float = 1.5
+    desc_scale_factor: float = 3.0
+    max_octaves: int = 0  # extension: 0 = reference formula
+
+    def to_c(self) -> CParams:
+        p = CParams()
+        for f in fields(self):
+            v = getattr(self, f.name)
+            setattr(p, f.name, int(v) if isinstance(v, bool) else v)
+        p.write_keypoints_png = 0
+        return p
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libsift_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} not found: build it with `make -C sift-project_amd` "
+            "(no CPU fallback exists on the product path)"
+        )
+    lib = ctypes.CDLL(path)
+    vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    lib.sift_params_default.argtypes = [ctypes.POINTER(CParams)]
+    lib.sift_hip_create.argtypes = [i, ctypes.POINTER(vp)]
+    lib.sift_hip_destroy.argtypes = [vp]
+    det_args = [vp, vp, i, i, i, ctypes.POINTER(CParams), ctypes.POINTER(vp),
+                ctypes.POINTER(sz), ctypes.POINTER(vp)]
+    lib.sift_hip_detect.argtypes = det_args
+    lib.sift_hip_detect_device.argtypes = det_args
+    lib.sift_hip_free.argtypes = [vp]
+    lib.sift_hip_free.restype = None
+    lib.sift_hip_strerror.argtypes = [i]
+    lib.sift_hip_strerror.restype = ctypes.c_char_p
+    lib.sift_hip_last_counts.argtypes = [vp, ctypes.POINTER(CCounts)]
+    lib.sift_hip_copy_level.argtypes = [vp, i, i, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
+    lib.sift_hip_copy_extrema.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    lib.sift_hip_copy_records_device.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    lib.sift_hip_stream.argtypes = [vp]
+    lib.sift_hip_stream.restype = vp
+    lib.sift_hip_set_profiling.argtypes = [vp, i]
+    lib.sift_hip_blur_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.POINTER(ctypes.c_double), i]
+    lib.sift_synth_image.argtypes = [i, i, i, ctypes.c_int64, ctypes.c_double,
+                                     ctypes.c_uint64, vp]
+    _lib = lib
+    return lib
+
+
+def _check(st: int) -> None:
+    if st != 0:
+        msg = load_library().sift_hip_strerror(st).decode()
+        raise RuntimeError(f"sift_hip error {st}: {msg}")
+
+
+def synth_image(w: int, h: int, channels: int = 1, nblobs: int | None = None,
+                smax: float = 6.0, seed: int = 42) -> np.ndarray:
+    """Deterministic synthetic image (HWC float64, values 0..255)."""
+    lib = load_library()
+    if nblobs is None:
+        nblobs = max(1, (w * h) // 52)  # 1080p -> ~40k blobs
+    out = np.empty((h, w, channels) if channels > 1 else (h, w), dtype=np.float64)
+    _check(lib.sift_synth_image(w, h, channels, nblobs, smax, seed, out.ctypes.data))
+    return out
+
+
+def _as_hwc(img: np.ndarray):
+    a = np.ascontiguousarray(img, dtype=np.float64)
+    if a.ndim == 2:
+        return a, a.shape[1], a.shape[0], 1
+    if a.ndim == 3:
+        return a, a.shape[1], a.shape[0], a.shape[2]
+    raise ValueError("image must be (H, W) or (H, W, C)")
+
+
+class Context:
+    """One HIP device context (stream + device arena)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self._ctx = ctypes.c_void_p()
+        _check(self.lib.sift_hip_create(device, ctypes.byref(self._ctx)))
+        self.device = device
+
+    def close(self) -> None:
+        if self._ctx:
+            self.lib.sift_hip_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _finish(self, kp_ptr, n, df_ptr, want_f32):
+        n = n.value
+        try:
+            kps = np.frombuffer(ctypes.string_at(kp_ptr.value, n * 168), dtype=KP_DTYPE).copy() \
+                if n else np.zeros(0, dtype=KP_DTYPE)
+            df = None
+            if want_f32:
+                df = np.frombuffer(ctypes.string_at(df_ptr.value, n * 512), dtype="<f4") \
+                    .reshape(n, 128).copy() if n else np.zeros((0, 128), np.float32)
+        finally:
+            self.lib.sift_hip_free(kp_ptr)
+            if want_f32:
+                self.lib.sift_hip_free(df_ptr)
+        return kps, df
+
+    def detect(self, img: np.ndarray, params: SiftParams | None = None, desc_f32: bool = False):
+        """detect_keypoints_and_descriptors on a host image (H,W[,C] float64)."""
+        a, w, h, c = _as_hwc(img)
+        p = (params or SiftParams()).to_c()
+        kp_ptr, n, df_ptr = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p()
+        _check(self.lib.sift_hip_detect(self._ctx, a.ctypes.data, w, h, c, ctypes.byref(p),
+                                        ctypes.byref(kp_ptr), ctypes.byref(n),
+                                        ctypes.byref(df_ptr) if desc_f32 else None))
+        return self._finish(kp_ptr, n, df_ptr, desc_f32)
+
+    def detect_device(self, dev_ptr: int, w: int, h: int, c: int = 1,
+                      params: SiftParams | None = None, desc_f32: bool = False):
+        """Same, with the image already resident in HBM (device pointer)."""
+        p = (params or SiftParams()).to_c()
+        kp_ptr, n, df_ptr = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p()
+        _check(self.lib.sift_hip_detect_device(self._ctx, ctypes.c_void_p(dev_ptr), w, h, c,
+                                               ctypes.byref(p), ctypes.byref(kp_ptr),
+                                               ctypes.byref(n),
+                                               ctypes.byref(df_ptr) if desc_f32 else None))
+        return self._finish(kp_ptr, n, df_ptr, desc_f32)
+
+    def counts(self) -> dict:
+        c = CCounts()
+        _check(self.lib.sift_hip_last_counts(self._ctx, ctypes.byref(c)))
+        return {f[0]: getattr(c, f[0]) for f in CCounts._fields_}
+
+    def level(self, octave: int, level: int) -> np.ndarray:
+        c = self.counts()
+        cap = c["octave0_w"] * c["octave0_h"]
+        buf = np.empty(cap, dtype=np.float64)
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.sift_hip_copy_level(self._ctx, octave, level, buf.ctypes.data, cap,
+                                            ctypes.byref(w), ctypes.byref(h)))
+        return buf[: w.value * h.value].reshape(h.value, w.value).copy()
+
+    def extrema(self) -> np.ndarray:
+        n = ctypes.c_size_t()
+        _check(self.lib.sift_hip_copy_extrema(self._ctx, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=EXT_DTYPE)
+        if n.value:
+            _check(self.lib.sift_hip_copy_extrema(self._ctx, out.ctypes.data, n.value,
+                                                  ctypes.byref(n)))
+        return out
+
+    def copy_records_device(self, dev_ptr: int, cap: int) -> int:
+        n = ctypes.c_size_t()
+        _check(self.lib.sift_hip_copy_records_device(self._ctx, ctypes.c_void_p(dev_ptr), cap,
+                                                     ctypes.byref(n)))
+        return n.value
+
+    def n_records(self) -> int:
+        n = ctypes.c_size_t()
+        _check(self.lib.sift_hip_copy_records_device(self._ctx, None, 0, ctypes.byref(n)))
+        return n.value
+
+    @property
+    def stream(self) -> int:
+        return self.lib.sift_hip_stream(self._ctx) or 0
+
+    def set_profiling(self, on: bool) -> None:
+        _check(self.lib.sift_hip_set_profiling(self._ctx, 1 if on else 0))
+
+    def blur_profile(self, reset: bool = False):
+        ms, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        _check(self.lib.sift_hip_blur_profile(self._ctx, ctypes.byref(ms), ctypes.byref(n),
+                                              ctypes.byref(b), 1 if reset else 0))
+        return ms.value, n.value, b.value
+
+
+def detect_keypoints_and_descriptors(img: np.ndarray, double_image_size: bool = True,
+                                     init_sigma: float = 1.6, intervals: int = 3,
+                                     window_size: int = 3, contrast_threshold: float = 0.04,
+                                     eigen_ratio: float = 10.0, num_bins: float = 36,
+                                     peak_ratio: float = 0.8, ori_sigma_factor: float = 1.5,
+                                     desc_scale_factor: float = 3.0, device: int = 0):
+    """Functional mirror of the reference entry point (sift.hh:65-71)."""
+    ctx = _default_context(device)
+    p = SiftParams(double_image_size, init_sigma, intervals, window_size, contrast_threshold,
+                   eigen_ratio, num_bins, peak_ratio, ori_sigma_factor, desc_scale_factor)
+    kps, _ = ctx.detect(img, p)
+    return kps
+
+
+_contexts: dict = {}
+
+
+def _default_context(device: int) -> Context:
+    if device not in _contexts:
+        _contexts[device] = Context(device)
+    return _contexts[device]
