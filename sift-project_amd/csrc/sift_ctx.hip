@@ -17,9 +17,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
-#include <numeric>
 #include <vector>
 
+#include "sift_host.h"
 #include "sift_kernels.h"
 
 using namespace sift_amd;
@@ -104,34 +104,6 @@ int ensure_t(T** p, unsigned* cap, unsigned need) {
     return SIFT_OK;
 }
 
-// apply_gaussian_blur_fast kernel construction (image.cpp:226-235) and the
-// running sum_w of apply_double_convolution_1d (image.cpp:171-185).
-bool make_taps(double sigma, BlurTaps* t) {
-    const double ks_d = std::ceil(3 * sigma);
-    if (!(ks_d >= 0) || ks_d + 1 > kMaxTaps) return false;
-    const int ks = (int)ks_d + 1;
-    std::memset(t, 0, sizeof *t);
-    const double exp_denom = 2 * sigma * sigma;
-    const double coef = 1 / (std::sqrt(2 * M_PI) * sigma);
-    for (int i = 0; i < ks; ++i) t->k[i] = std::exp(-i * i / exp_denom) * coef;
-    double s = t->k[0];
-    for (int u = 1; u < ks; ++u) s += 2.0 * t->k[u];
-    t->sum_w = s;
-    t->R = ks - 1;
-    return true;
-}
-
-bool kp_less(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator<, sift.hh:31-41
-    if (a.x != b.x) return a.x < b.x;
-    if (a.y != b.y) return a.y < b.y;
-    if (a.size != b.size) return a.size > b.size;
-    if (a.pori != b.pori) return a.pori < b.pori;
-    return a.octave > b.octave;
-}
-bool kp_equal(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator==, sift.hh:25-27
-    return a.x == b.x && a.y == b.y && a.size == b.size && a.pori == b.pori;
-}
-
 hipEvent_t next_event(sift_ctx* ctx) {
     if (ctx->ev_used == ctx->ev_pool.size()) {
         hipEvent_t e;
@@ -139,87 +111,6 @@ hipEvent_t next_event(sift_ctx* ctx) {
         ctx->ev_pool.push_back(e);
     }
     return ctx->ev_pool[ctx->ev_used++];
-}
-
-struct Geometry {
-    int octaves = 0;
-    int n_gauss = 0;
-    int W[kMaxOctaves] = {0};
-    int H[kMaxOctaves] = {0};
-    size_t offs[kMaxOctaves][kMaxLevels] = {{0}};
-    size_t total = 0;   // doubles in the pyramid
-    size_t sum_px = 0;  // sum over octaves of W*H
-};
-
-int plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* taps_init,
-         BlurTaps* taps, DevParams* dp) {
-    if (w <= 0 || h <= 0) return SIFT_ERR_ARG;
-    if (c != 1 && c != 3) return SIFT_ERR_CHANNELS;
-    if (p->intervals < 1 || p->intervals + 3 > kMaxLevels) return SIFT_ERR_PARAM;
-    if (p->window_size < 2 || p->window_size / 2 > 3) return SIFT_ERR_PARAM;
-    const int nb = (int)p->num_bins;
-    if (nb < 1 || nb > kMaxBins) return SIFT_ERR_PARAM;
-    if (!(p->init_sigma * p->init_sigma - 1 > 0)) return SIFT_ERR_PARAM;
-    if (p->max_octaves < 0) return SIFT_ERR_PARAM;
-
-    const int W0 = p->double_image_size ? 2 * w : w;
-    const int H0 = p->double_image_size ? 2 * h : h;
-    // compute_octaves_count (sift.cpp:132-137), integer division by 3
-    const int q = std::min(W0, H0) / 3;
-    if (q == 0) return SIFT_ERR_TOO_SMALL;
-    int octaves = (int)std::floor(std::log2(q));
-    if (p->max_octaves > 0 && octaves > p->max_octaves) octaves = p->max_octaves;
-    if (octaves < 1 || octaves > kMaxOctaves) return SIFT_ERR_TOO_SMALL;
-    g->octaves = octaves;
-    g->n_gauss = p->intervals + 3;
-    int Wo = W0, Ho = H0;
-    size_t off = 0;
-    for (int o = 0; o < octaves; ++o) {
-        // the reference decimates after every octave and throws when the
-        // level is smaller than 2x2 (image.cpp:42-44, sift.cpp:195)
-        if (Wo < 2 || Ho < 2) return SIFT_ERR_TOO_SMALL;
-        g->W[o] = Wo;
-        g->H[o] = Ho;
-        g->sum_px += (size_t)Wo * Ho;
-        for (int l = 0; l < g->n_gauss; ++l) {
-            g->offs[o][l] = off;
-            off += (size_t)Wo * Ho;
-        }
-        Wo /= 2;
-        Ho /= 2;
-    }
-    g->total = off;
-
-    // compute_gaussian_kernels (sift.cpp:143-155)
-    std::vector<double> sig(g->n_gauss);
-    sig[0] = p->init_sigma;
-    const double k = std::pow(2.0, 1.0 / p->intervals);
-    for (int i = 1; i < g->n_gauss; ++i) {
-        const double prev = (std::pow(k, i - 1)) * p->init_sigma;
-        sig[i] = prev * std::sqrt(k * k - 1);
-    }
-    if (!make_taps(std::sqrt(p->init_sigma * p->init_sigma - 1), taps_init))
-        return SIFT_ERR_PARAM;
-    for (int i = 1; i < g->n_gauss; ++i)
-        if (!make_taps(sig[i], &taps[i])) return SIFT_ERR_PARAM;
-
-    dp->intervals = p->intervals;
-    dp->window_size = p->window_size;
-    dp->num_bins = nb;
-    dp->double_image = p->double_image_size ? 1 : 0;
-    // detect_extrema: double threshold passed into an int (sift.cpp:266,305-307)
-    dp->threshold = (int)std::floor(0.5 * p->contrast_threshold /
-                                    static_cast<double>(p->intervals) * 255.0);
-    dp->n_dog = p->intervals + 2;
-    dp->n_gauss = g->n_gauss;
-    dp->octaves = octaves;
-    dp->init_sigma = p->init_sigma;
-    dp->contrast_threshold = p->contrast_threshold;
-    dp->eigen_ratio = p->eigen_ratio;
-    dp->peak_ratio = p->peak_ratio;
-    dp->ori_sigma_factor = p->ori_sigma_factor;
-    dp->desc_scale_factor = p->desc_scale_factor;
-    return SIFT_OK;
 }
 
 int blur_launch(sift_ctx* ctx, const double* src, double* dst, int W, int H,
@@ -251,7 +142,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     BlurTaps taps_init;
     std::vector<BlurTaps> taps(kMaxLevels);
     DevParams dp;
-    int st = plan(p, w, h, c, &g, &taps_init, taps.data(), &dp);
+    int st = host_plan(p, w, h, c, &g, &taps_init, taps.data(), &dp);
     if (st != SIFT_OK) return st;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
     ctx->have_run = false;
@@ -367,28 +258,9 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         ctx->pending.clear();
     }
 
-    // final size with glibc pow (sift.cpp:427-429, halved at sift.cpp:525)
-    for (unsigned i = 0; i < n_ori; ++i) {
-        sift_kp& r = ctx->h_ori[i];
-        const double scale = std::pow(2, r.octave);
-        double size = p->init_sigma * scale *
-                      std::pow(2, (static_cast<double>(r.layer) + ctx->h_off0[i]) / p->intervals);
-        if (p->double_image_size) size /= 2;
-        r.size = size;
-    }
-    // clean_keypoints (sift.cpp:20-24): sort then unique on (x, y, size, pori)
-    std::vector<unsigned> idx(n_ori);
-    std::iota(idx.begin(), idx.end(), 0u);
-    std::sort(idx.begin(), idx.end(), [&](unsigned a, unsigned b) {
-        return kp_less(ctx->h_ori[a], ctx->h_ori[b]);
-    });
-    std::vector<unsigned> keep;
-    keep.reserve(n_ori);
-    for (unsigned i = 0; i < n_ori; ++i)
-        if (keep.empty() || !kp_equal(ctx->h_ori[keep.back()], ctx->h_ori[idx[i]]))
-            keep.push_back(idx[i]);
-
-    const size_t n = keep.size();
+    // final size with glibc pow + clean_keypoints, in the g++-built layer
+    std::vector<unsigned> keep(n_ori);
+    const size_t n = host_finalize(p, ctx->h_ori.data(), ctx->h_off0.data(), n_ori, keep.data());
     sift_kp* kps = (sift_kp*)std::malloc(std::max<size_t>(n, 1) * sizeof(sift_kp));
     if (!kps) return SIFT_ERR_NOMEM;
     for (size_t i = 0; i < n; ++i) kps[i] = ctx->h_ori[keep[i]];

@@ -1,0 +1,141 @@
+// sift_host.cpp — glibc-exact host math of the pipeline (see sift_host.h).
+// Built with g++ -ffp-contract=off, never with hipcc/clang.
+#include "sift_host.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+namespace sift_amd {
+
+namespace {
+
+// apply_gaussian_blur_fast kernel construction (image.cpp:226-235) and the
+// running sum_w of apply_double_convolution_1d (image.cpp:171-185), which is
+// the same sequence for every pixel and therefore a per-kernel constant.
+bool make_taps(double sigma, BlurTaps* t) {
+    const double ks_d = std::ceil(3 * sigma);
+    if (!(ks_d >= 0) || ks_d + 1 > kMaxTaps) return false;
+    const int ks = (int)ks_d + 1;
+    std::memset(t, 0, sizeof *t);
+    const double exp_denom = 2 * sigma * sigma;
+    const double coef = 1 / (std::sqrt(2 * M_PI) * sigma);
+    for (int i = 0; i < ks; ++i) t->k[i] = std::exp(-i * i / exp_denom) * coef;
+    double s = t->k[0];
+    for (int u = 1; u < ks; ++u) s += 2.0 * t->k[u];
+    t->sum_w = s;
+    t->R = ks - 1;
+    return true;
+}
+
+bool kp_less(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator<, sift.hh:31-41
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.pori != b.pori) return a.pori < b.pori;
+    return a.octave > b.octave;
+}
+
+bool kp_equal(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator==, sift.hh:25-27
+    return a.x == b.x && a.y == b.y && a.size == b.size && a.pori == b.pori;
+}
+
+}  // namespace
+
+int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* taps_init,
+              BlurTaps* taps, DevParams* dp) {
+    if (w <= 0 || h <= 0) return SIFT_ERR_ARG;
+    if (c != 1 && c != 3) return SIFT_ERR_CHANNELS;
+    if (p->intervals < 1 || p->intervals + 3 > kMaxLevels) return SIFT_ERR_PARAM;
+    if (p->window_size < 2 || p->window_size / 2 > 3) return SIFT_ERR_PARAM;
+    const int nb = (int)p->num_bins;
+    if (nb < 1 || nb > kMaxBins) return SIFT_ERR_PARAM;
+    if (!(p->init_sigma * p->init_sigma - 1 > 0)) return SIFT_ERR_PARAM;
+    if (p->max_octaves < 0) return SIFT_ERR_PARAM;
+
+    const int W0 = p->double_image_size ? 2 * w : w;
+    const int H0 = p->double_image_size ? 2 * h : h;
+    // compute_octaves_count (sift.cpp:132-137): integer division by 3
+    const int q = std::min(W0, H0) / 3;
+    if (q == 0) return SIFT_ERR_TOO_SMALL;
+    int octaves = std::floor(std::log2(q));
+    if (p->max_octaves > 0 && octaves > p->max_octaves) octaves = p->max_octaves;
+    if (octaves < 1 || octaves > kMaxOctaves) return SIFT_ERR_TOO_SMALL;
+    *g = Geometry();
+    g->octaves = octaves;
+    g->n_gauss = p->intervals + 3;
+    int Wo = W0, Ho = H0;
+    size_t off = 0;
+    for (int o = 0; o < octaves; ++o) {
+        // the reference decimates after every octave and throws below 2x2
+        // (image.cpp:42-44, sift.cpp:195)
+        if (Wo < 2 || Ho < 2) return SIFT_ERR_TOO_SMALL;
+        g->W[o] = Wo;
+        g->H[o] = Ho;
+        g->sum_px += (size_t)Wo * Ho;
+        for (int l = 0; l < g->n_gauss; ++l) {
+            g->offs[o][l] = off;
+            off += (size_t)Wo * Ho;
+        }
+        Wo /= 2;
+        Ho /= 2;
+    }
+    g->total = off;
+
+    // compute_gaussian_kernels (sift.cpp:143-155)
+    std::vector<double> sig(g->n_gauss);
+    sig[0] = p->init_sigma;
+    const double k = std::pow(2.0, 1.0 / p->intervals);
+    for (int i = 1; i < g->n_gauss; ++i) {
+        const double prev = (std::pow(k, i - 1)) * p->init_sigma;
+        sig[i] = prev * std::sqrt(k * k - 1);
+    }
+    // compute_initial_image's blur sigma (sift.cpp:124)
+    if (!make_taps(std::sqrt(p->init_sigma * p->init_sigma - 1), taps_init))
+        return SIFT_ERR_PARAM;
+    for (int i = 1; i < g->n_gauss; ++i)
+        if (!make_taps(sig[i], &taps[i])) return SIFT_ERR_PARAM;
+
+    dp->intervals = p->intervals;
+    dp->window_size = p->window_size;
+    dp->num_bins = nb;
+    dp->double_image = p->double_image_size ? 1 : 0;
+    // detect_extrema: the double threshold is passed into an int parameter
+    // (sift.cpp:266, 305-307)
+    dp->threshold = (int)std::floor(0.5 * p->contrast_threshold /
+                                    static_cast<double>(p->intervals) * 255.0);
+    dp->n_dog = p->intervals + 2;
+    dp->n_gauss = g->n_gauss;
+    dp->octaves = octaves;
+    dp->init_sigma = p->init_sigma;
+    dp->contrast_threshold = p->contrast_threshold;
+    dp->eigen_ratio = p->eigen_ratio;
+    dp->peak_ratio = p->peak_ratio;
+    dp->ori_sigma_factor = p->ori_sigma_factor;
+    dp->desc_scale_factor = p->desc_scale_factor;
+    return SIFT_OK;
+}
+
+size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
+                     unsigned* keep) {
+    for (unsigned i = 0; i < n; ++i) {
+        sift_kp& r = recs[i];
+        const double scale = std::pow(2, r.octave);
+        double size = p->init_sigma * scale *
+                      std::pow(2, (static_cast<double>(r.layer) + off0[i]) / p->intervals);
+        if (p->double_image_size) size /= 2;
+        r.size = size;
+    }
+    std::vector<unsigned> idx(n);
+    std::iota(idx.begin(), idx.end(), 0u);
+    std::sort(idx.begin(), idx.end(),
+              [&](unsigned a, unsigned b) { return kp_less(recs[a], recs[b]); });
+    size_t m = 0;
+    for (unsigned i = 0; i < n; ++i)
+        if (m == 0 || !kp_equal(recs[keep[m - 1]], recs[idx[i]])) keep[m++] = idx[i];
+    return m;
+}
+
+}  // namespace sift_amd

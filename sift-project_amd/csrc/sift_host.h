@@ -1,0 +1,38 @@
+// sift_host.h — host-side reference math of the pipeline (sift_host.cpp).
+//
+// Everything here is computed with glibc libm in the reference's expression
+// order and must be compiled with g++ (like the reference, Makefile:2,5):
+// clang/LLVM rewrites pow(2.0, x) into exp2(x) even without fast-math, and
+// glibc's exp2 and pow disagree in the last bit for rare arguments.
+#pragma once
+
+#include <cstddef>
+
+#include "sift_types.h"
+
+namespace sift_amd {
+
+struct Geometry {
+    int octaves = 0;
+    int n_gauss = 0;
+    int W[kMaxOctaves] = {0};
+    int H[kMaxOctaves] = {0};
+    size_t offs[kMaxOctaves][kMaxLevels] = {{0}};
+    size_t total = 0;   // doubles in the pyramid
+    size_t sum_px = 0;  // sum over octaves of W*H
+};
+
+// Octave geometry (sift.cpp:132-137, image.cpp:41-45), level sigmas
+// (sift.cpp:143-155), blur taps (image.cpp:226-235), extremum threshold
+// (sift.cpp:305-307) and parameter validation.
+int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* taps_init,
+              BlurTaps* taps, DevParams* dp);
+
+// Final keypoint size with glibc pow (sift.cpp:427-429, halved at
+// sift.cpp:525) written into recs[i].size, then clean_keypoints
+// (sift.cpp:20-24): indices of the sorted, de-duplicated records go to keep[]
+// (capacity n). Returns the number kept.
+size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
+                     unsigned* keep);
+
+}  // namespace sift_amd

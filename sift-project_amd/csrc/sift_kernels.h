@@ -6,66 +6,9 @@
 
 #include <cstdint>
 
-#include "../../include/sift_hip.h"
+#include "sift_types.h"
 
 namespace sift_amd {
-
-// Algorithm constants of the reference (sift.hh:5-13).
-constexpr int kMaxSteps = 5;        // MAX_CONVERGENCE_STEPS
-constexpr double kConvThr = 0.5;    // CONVERGENCE_THR
-constexpr int kSmoothIters = 2;     // ORI_SMOOTH_ITERATIONS
-constexpr int kDescW = 4;           // DESC_HIST_WIDTH
-constexpr int kDescBins = 8;        // DESC_HIST_BINS
-constexpr double kMagThr = 0.2;     // DESC_MAGNITUDE_THR
-constexpr double kIntFactor = 512.0;  // INT_DESCR_FCTR
-
-constexpr int kMaxOctaves = 16;   // floor(log2(min/3)) < 16 for any int image
-constexpr int kMaxLevels = 12;    // intervals + 3 with intervals <= 9
-constexpr int kMaxTemplR = 24;    // widest register-window blur kernel
-constexpr int kMaxTaps = 64;      // generic path: kernels up to 64 taps
-constexpr int kMaxBins = 256;     // orientation bins supported
-
-// Half kernel of apply_gaussian_blur_fast (image.cpp:226-235) plus its
-// normalising sum (image.cpp:171-185), computed on the host with glibc.
-struct BlurTaps {
-    double k[kMaxTaps];
-    double sum_w;
-    int R;  // taps k[0..R], R = ks-1
-    int pad;
-};
-
-// Device-resident table of pyramid level planes.
-struct PyrTable {
-    double* lvl[kMaxOctaves][kMaxLevels];
-    int w[kMaxOctaves];
-    int h[kMaxOctaves];
-};
-
-// Scalar parameters of detect_keypoints_and_descriptors as the kernels need
-// them (sift.hh:65-71, threshold per sift.cpp:305-307).
-struct DevParams {
-    int intervals;
-    int window_size;
-    int num_bins;
-    int double_image;
-    int threshold;
-    int n_dog;
-    int n_gauss;
-    int octaves;
-    double init_sigma;
-    double contrast_threshold;
-    double eigen_ratio;
-    double peak_ratio;
-    double ori_sigma_factor;
-    double desc_scale_factor;
-};
-
-// Refined keypoint before orientation (sift.cpp:419-430) plus the scale
-// offset, which the host needs to recompute size with glibc pow.
-struct RawKp {
-    double x, y, size, off0;
-    int octave, layer;
-};
 
 int blur_rows_for(int W, int H, int R);
 

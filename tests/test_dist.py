@@ -1,0 +1,65 @@
+"""CPU: the multi-GPU batch path (image sharding + all-gather of descriptor
+buffers) with torch.distributed gloo, world_size 2 and 3."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle_bind import OracleRun
+from sift_dist import RECORD_BYTES, allgather_records, shard
+from sift_hip import synth_image
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_images, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = shard(n_images, rank, world)
+        max_local = (n_images + world - 1) // world
+        bufs = []
+        for i in mine:
+            # the CPU oracle stands in for the GPU detect on this CPU test
+            img = synth_image(96, 72, 1, seed=1000 + i)
+            fin = OracleRun(img).final
+            bufs.append(torch.from_numpy(np.frombuffer(fin.tobytes(), np.uint8)
+                                         .reshape(-1, RECORD_BYTES).copy()))
+        got = allgather_records(bufs, mine, max_local)
+        out_q.put((rank, {k: v.numpy().tobytes() for k, v in got.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_images", [(2, 5), (3, 7), (2, 2)])
+def test_allgather_records_gloo(world, n_images):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_images, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = {i: OracleRun(synth_image(96, 72, 1, seed=1000 + i)).final.tobytes()
+              for i in range(n_images)}
+    for r in range(world):
+        assert results[r] == expect
+
+
+def test_shard_is_a_partition():
+    for world in (1, 2, 4, 8):
+        seen = sorted(i for r in range(world) for i in shard(64, r, world))
+        assert seen == list(range(64))
+        assert all(len(shard(64, r, world)) == 64 // world for r in range(world))

@@ -1,0 +1,172 @@
+"""GPU: the HIP path through the C-ABI against the reference goldens and the
+oracle, stage by stage, plus edge cases and full-size properties.
+
+Tolerances (tests/parity.py): pyramid levels, extrema set, final count and
+x/y/octave/layer/size bit-exact; pori <= 1e-9; normalised descriptor floats
+<= 1e-4; u8 descriptors +-1 on at most 0.1% of bytes.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from golden_util import all_goldens, sha256_array
+from oracle_bind import OracleRun
+from parity import compare_final, final_ok, sort_extrema
+from sift_hip import EXT_DTYPE, SiftParams, synth_image
+
+pytestmark = pytest.mark.gpu
+
+GOLDENS = all_goldens(kinds=("small", "medium"))
+BIG = all_goldens(kinds=("big",))
+
+
+def _golden_extrema(g):
+    ge = np.zeros(len(g.extrema), dtype=EXT_DTYPE)
+    for i, f in enumerate(("x", "y", "z", "octave")):
+        ge[f] = g.extrema[:, i]
+    return sort_extrema(ge)
+
+
+@pytest.mark.parametrize("g", GOLDENS, ids=[g.name for g in GOLDENS])
+def test_gpu_matches_reference_golden(gpu_ctx, g):
+    img = g.input()
+    kps, df = gpu_ctx.detect(img, g.params(), desc_f32=True)
+    c = gpu_ctx.counts()
+    m = g.meta
+    assert (c["octaves"], c["extrema"], c["refined"], c["oriented"], c["final_n"]) == \
+        (m["octaves"], m["extrema"], m["refined"], m["oriented"], m["final"])
+    assert np.array_equal(sort_extrema(gpu_ctx.extrema()), _golden_extrema(g))
+    r = compare_final(kps, df, g.final, g.desc_f32)
+    assert final_ok(r), r
+    if g.pyr_sha256 is not None:
+        hashes = g.level_hashes()
+        for o in range(m["octaves"]):
+            for lv in range(m["levels"]):
+                assert sha256_array(gpu_ctx.level(o, lv)) == hashes[o][lv], (o, lv)
+
+
+@pytest.mark.parametrize("g", BIG, ids=[g.name for g in BIG])
+def test_gpu_matches_big_golden_sample(gpu_ctx, g):
+    img = g.input()
+    kps, df = gpu_ctx.detect(img, g.params(), desc_f32=True)
+    c = gpu_ctx.counts()
+    m = g.meta
+    assert (c["extrema"], c["refined"], c["final_n"]) == (m["extrema"], m["refined"], m["final"])
+    assert sha256_array(sort_extrema(gpu_ctx.extrema()).view("<i4")) == m["extrema_sha256"]
+    sub = kps[g.sample_idx]
+    r = compare_final(sub, df[g.sample_idx], g.final, g.desc_f32)
+    assert final_ok(r), r
+
+
+CASES = [
+    ("ragged_67x43", 67, 43, 1, SiftParams()),
+    ("rgb_203x151", 203, 151, 3, SiftParams()),
+    ("nodbl_rgb_250x190", 250, 190, 3, SiftParams(double_image_size=False)),
+    ("int4_180x140", 180, 140, 1, SiftParams(intervals=4)),
+    ("int1_150x110", 150, 110, 1, SiftParams(intervals=1)),
+    ("win5_170x130", 170, 130, 1, SiftParams(window_size=5)),
+    ("bins72_160x120", 160, 120, 1, SiftParams(num_bins=72, peak_ratio=0.5)),
+    ("lowthr_160x120", 160, 120, 1, SiftParams(contrast_threshold=0.02, eigen_ratio=5.0)),
+    ("oridesc_160x120", 160, 120, 1, SiftParams(ori_sigma_factor=2.0, desc_scale_factor=4.0)),
+    ("sigma2_140x100", 140, 100, 1, SiftParams(init_sigma=2.0)),
+    ("wide_sigma_90x70", 90, 70, 1, SiftParams(init_sigma=6.5)),  # R > 24: generic blur path
+    ("maxoct3_300x220", 300, 220, 1, SiftParams(max_octaves=3)),
+    ("tall_33x400", 33, 400, 1, SiftParams()),
+    ("wide_600x20", 600, 20, 1, SiftParams()),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_gpu_matches_oracle_stagewise(gpu_ctx, case):
+    name, w, h, c, p = case
+    img = synth_image(w, h, c, seed=zlib.crc32(name.encode()) & 0xFFFF)
+    ref = OracleRun(img, p)
+    kps, df = gpu_ctx.detect(img, p, desc_f32=True)
+    cnt = gpu_ctx.counts()
+    for o in range(ref.octaves):
+        for lv in range(ref.levels):
+            a, b = gpu_ctx.level(o, lv), ref.level(o, lv)
+            assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (o, lv)
+    assert np.array_equal(sort_extrema(gpu_ctx.extrema()), sort_extrema(ref.extrema))
+    assert cnt["refined"] == len(ref.refined)
+    assert cnt["oriented"] == len(ref.oriented)
+    r = compare_final(kps, df, ref.final, ref.desc_f32)
+    assert final_ok(r), r
+
+
+def test_gpu_flat_and_tiny_images(gpu_ctx):
+    kps, _ = gpu_ctx.detect(np.full((64, 80), 77.0))
+    assert len(kps) == 0 and gpu_ctx.counts()["extrema"] == 0
+    kps, _ = gpu_ctx.detect(synth_image(5, 4, 1, nblobs=2, smax=1.0, seed=2))
+    assert gpu_ctx.counts()["octaves"] == 1
+
+
+def test_gpu_error_paths(gpu_ctx):
+    with pytest.raises(RuntimeError, match="too small"):
+        gpu_ctx.detect(np.zeros((1, 1)))
+    with pytest.raises(RuntimeError, match="channel"):
+        gpu_ctx.detect(np.zeros((16, 16, 2)))
+    with pytest.raises(RuntimeError, match="parameter"):
+        gpu_ctx.detect(np.zeros((32, 32)), SiftParams(intervals=0))
+    with pytest.raises(RuntimeError, match="parameter"):
+        gpu_ctx.detect(np.zeros((32, 32)), SiftParams(window_size=1))
+    # the context stays usable after errors
+    kps, _ = gpu_ctx.detect(synth_image(64, 48, 1, seed=42))
+    assert len(kps) > 0
+
+
+def test_gpu_deterministic_and_device_input(gpu_ctx):
+    import torch
+
+    img = synth_image(640, 480, 1, seed=123)
+    a, da = gpu_ctx.detect(img, desc_f32=True)
+    b, db = gpu_ctx.detect(img, desc_f32=True)
+    assert a.tobytes() == b.tobytes() and np.array_equal(da, db)
+    t = torch.from_numpy(img).to("cuda:0")
+    torch.cuda.synchronize()
+    c, dc = gpu_ctx.detect_device(t.data_ptr(), 640, 480, 1, desc_f32=True)
+    assert a.tobytes() == c.tobytes() and np.array_equal(da, dc)
+
+
+def test_gpu_capacity_regrowth(gpu_ctx):
+    # a dense small image after a large one exercises arena reuse; a dense
+    # large one exercises overflow re-runs of the compaction buffers
+    img = synth_image(1024, 768, 1, nblobs=60000, smax=2.0, seed=77)
+    ref = OracleRun(img)
+    kps, df = gpu_ctx.detect(img, desc_f32=True)
+    assert final_ok(compare_final(kps, df, ref.final, ref.desc_f32))
+
+
+@pytest.mark.slow
+def test_gpu_8k_properties(gpu_ctx):
+    """BASELINE config 5 (7680x4320, dense): size-independent properties."""
+    img = synth_image(7680, 4320, 1, nblobs=1500000, smax=4.0, seed=42)
+    kps, df = gpu_ctx.detect(img, desc_f32=True)
+    c = gpu_ctx.counts()
+    assert c["octaves"] == 11 and c["final_n"] == len(kps) > 100000
+    # clean_keypoints order and uniqueness
+    order = np.lexsort((-kps["octave"], kps["pori"], -kps["size"], kps["y"], kps["x"]))
+    assert np.array_equal(order, np.arange(len(kps)))
+    # keypoints inside the input image, orientations in [0, 2pi)
+    assert kps["x"].min() >= 0 and kps["x"].max() < 7680
+    assert kps["y"].min() >= 0 and kps["y"].max() < 4320
+    assert kps["pori"].min() >= 0 and kps["pori"].max() < 2 * np.pi
+    # descriptor floats: unit norm after the 0.2 clamp
+    nrm = np.linalg.norm(df.astype(np.float64), axis=1)
+    nrm = nrm[~np.isnan(nrm)]  # all-zero histograms give NaN (Appendix A.17)
+    assert len(nrm) > 0.99 * len(kps) and np.all(np.abs(nrm - 1.0) < 1e-5)
+    # next-octave base == decimated level `intervals` (sift.cpp:195-196)
+    g3 = gpu_ctx.level(1, 3)
+    g0n = gpu_ctx.level(2, 0)
+    assert np.array_equal(g0n, g3[: g0n.shape[0] * 2: 2, : g0n.shape[1] * 2: 2])
+    # each sampled extremum satisfies the cube condition on the pyramid
+    ext = gpu_ctx.extrema()
+    o = 3
+    e = ext[ext["octave"] == o][:500]
+    G = [gpu_ctx.level(o, lv) for lv in range(6)]
+    D = [G[i + 1] - G[i] for i in range(5)]
+    for x, y, z, _ in e:
+        v = D[z][y, x]
+        cube = np.stack([D[z + dz][y - 1:y + 2, x - 1:x + 2] for dz in (-1, 0, 1)])
+        assert abs(v) > 1 and (v == cube.max() or v == cube.min())
