@@ -157,6 +157,12 @@ int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out,
 int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap,
                                  size_t* n_out);
 
+/* Host-side wall time (ms) of the phases of the last detect: [0] plan +
+ * enqueue of every kernel, [1] wait for the device pipeline, [2] download of
+ * the keypoint records, [3] final size + clean_keypoints, [4] output
+ * assembly. Writes min(n, 5) values. */
+int sift_hip_last_timing(sift_ctx* ctx, double* ms, int n);
+
 /* The context's HIP stream (hipStream_t), for event timing. */
 void* sift_hip_stream(sift_ctx* ctx);
 

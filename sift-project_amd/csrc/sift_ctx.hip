@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -25,6 +26,32 @@
 using namespace sift_amd;
 
 namespace {
+
+template <class T>
+struct Pinned {  // grow-only pinned host buffer (fast async D2H, no staging)
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (p && cap >= n) return SIFT_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = n < 1024 ? 1024 : n + n / 4;
+        if (hipHostMalloc(&p, want * sizeof(T)) != hipSuccess) return SIFT_ERR_NOMEM;
+        cap = want;
+        return SIFT_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Stage {
+    PyrTable pt;
+    BlurTaps taps[kMaxLevels];
+};
 
 struct EventPair {
     hipEvent_t a, b;
@@ -53,7 +80,11 @@ struct sift_ctx {
     unsigned* d_ctr = nullptr;
     unsigned* h_ctr = nullptr;  // pinned
     PyrTable h_pt{};
-    PyrTable* d_pt = nullptr;
+    // per-call tables: pinned host staging -> one async copy -> device
+    Stage* h_stage = nullptr;
+    Stage* d_stage = nullptr;
+    PyrTable* d_pt = nullptr;     // &d_stage->pt
+    BlurTaps* d_taps = nullptr;   // d_stage->taps
 
     // last detect
     bool have_run = false;
@@ -69,10 +100,16 @@ struct sift_ctx {
     int64_t prof_launches = 0;
     double prof_bytes = 0.0;
 
-    // host staging
-    std::vector<sift_kp> h_ori;
-    std::vector<double> h_off0;
-    std::vector<float> h_df32;
+    // host staging (pinned)
+    Pinned<sift_kp> h_ori;
+    Pinned<double> h_off0;
+    Pinned<float> h_df32;
+    std::vector<unsigned> keep;
+
+    // host-side phase wall times of the last detect (ms): enqueue, wait for
+    // the device pipeline, records download, finalize (size + sort/unique),
+    // output assembly
+    double t_host[5] = {0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -138,6 +175,11 @@ int blur_launch(sift_ctx* ctx, const double* src, double* dst, int W, int H,
 int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
                 const sift_params* p, sift_kp** out_kps, size_t* out_n,
                 float** out_desc_f32) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
     Geometry g;
     BlurTaps taps_init;
     std::vector<BlurTaps> taps(kMaxLevels);
@@ -156,7 +198,11 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         ctx->h_pt.h[o] = g.H[o];
         for (int l = 0; l < g.n_gauss; ++l) ctx->h_pt.lvl[o][l] = ctx->d_pyr + g.offs[o][l];
     }
-    SIFT_HIP_TRY(hipMemcpyAsync(ctx->d_pt, &ctx->h_pt, sizeof(PyrTable),
+    // the previous call's copy out of h_stage has completed (every detect
+    // ends with a stream synchronisation), so the staging can be rewritten
+    ctx->h_stage->pt = ctx->h_pt;
+    for (int l = 0; l < g.n_gauss; ++l) ctx->h_stage->taps[l] = taps[l];
+    SIFT_HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, sizeof(Stage),
                                 hipMemcpyHostToDevice, ctx->stream));
 
     // capacities for the variable-size stages; grown and re-run on overflow
@@ -185,7 +231,15 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     if ((st = blur_launch(ctx, base_src, G00, W0, H0, taps_init, nullptr, 0, 0)) != SIFT_OK)
         return st;
     const int dec_level = g.n_gauss - 3;  // = intervals (sift.cpp:195-196)
-    for (int o = 0; o < g.octaves; ++o) {
+    // octaves from o_small on are small enough to run LDS-resident in one
+    // launch (k_octaves_lds); the larger ones get one k_blur launch per level
+    int o_small = g.octaves;
+    for (int o = 0; o < g.octaves; ++o)
+        if ((size_t)g.W[o] * g.H[o] <= (size_t)kLdsOctavePx) {
+            o_small = o;
+            break;
+        }
+    for (int o = 0; o < o_small; ++o) {
         for (int l = 1; l < g.n_gauss; ++l) {
             const bool dec = (l == dec_level) && (o + 1 < g.octaves);
             st = blur_launch(ctx, ctx->h_pt.lvl[o][l - 1], ctx->h_pt.lvl[o][l], g.W[o], g.H[o],
@@ -194,14 +248,52 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             if (st != SIFT_OK) return st;
         }
     }
+    if (o_small < g.octaves) {
+        hipEvent_t ea = nullptr, eb = nullptr;
+        if (ctx->profiling) {
+            ea = next_event(ctx);
+            eb = next_event(ctx);
+            if (!ea || !eb) return SIFT_ERR_HIP;
+            SIFT_HIP_TRY(hipEventRecord(ea, ctx->stream));
+        }
+        SIFT_HIP_TRY(launch_octaves_lds(ctx->d_pt, o_small, g.octaves - 1, g.n_gauss,
+                                        ctx->d_taps, ctx->stream));
+        if (ctx->profiling) {
+            SIFT_HIP_TRY(hipEventRecord(eb, ctx->stream));
+            double bytes = 0.0;
+            for (int o = o_small; o < g.octaves; ++o) {
+                bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[o] * (double)g.H[o];
+                if (o + 1 < g.octaves) bytes += 8.0 * (double)g.W[o + 1] * (double)g.H[o + 1];
+            }
+            ctx->pending.push_back({ea, eb, bytes});
+        }
+    }
+
+    // extrema tile grid (window_size 3): every octave in one launch
+    ExtremaGrid eg;
+    std::memset(&eg, 0, sizeof eg);
+    eg.octaves = g.octaves;
+    for (int o = 0; o < g.octaves; ++o) {
+        const int tx = g.W[o] > 2 ? (g.W[o] - 2 + 63) / 64 : 0;
+        const int ty = g.H[o] > 2 ? (g.H[o] - 2 + 15) / 16 : 0;
+        eg.tiles_x[o] = tx > 0 ? tx : 1;
+        eg.first_tile[o + 1] = eg.first_tile[o] + tx * ty;
+    }
 
     // ---- extrema -> refine -> orientation -> descriptor, re-run on overflow
+    clk::time_point t_enq, t_wait;
     for (int attempt = 0;; ++attempt) {
         SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, 4 * sizeof(unsigned), ctx->stream));
-        for (int o = 0; o < g.octaves; ++o)
-            SIFT_HIP_TRY(launch_extrema(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
-                                        p->window_size, dp.threshold, ctx->d_cand,
-                                        ctx->d_ctr + 0, ctx->cap_cand, ctx->stream));
+        if (p->window_size / 2 == 1) {
+            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold,
+                                              ctx->d_cand, ctx->d_ctr + 0, ctx->cap_cand,
+                                              ctx->stream));
+        } else {
+            for (int o = 0; o < g.octaves; ++o)
+                SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
+                                                p->window_size, dp.threshold, ctx->d_cand,
+                                                ctx->d_ctr + 0, ctx->cap_cand, ctx->stream));
+        }
         SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, ctx->d_ctr + 0, ctx->cap_cand,
                                    ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, ctx->stream));
         SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw,
@@ -211,7 +303,9 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
                                        out_desc_f32 ? ctx->d_df32 : nullptr, ctx->stream));
         SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
                                     hipMemcpyDeviceToHost, ctx->stream));
+        t_enq = clk::now();
         SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+        t_wait = clk::now();
         const unsigned nc = ctx->h_ctr[0], nr = ctx->h_ctr[1], no = ctx->h_ctr[2];
         if (nc <= ctx->cap_cand && nr <= ctx->cap_raw && no <= ctx->cap_ori) break;
         if (attempt >= 3) return SIFT_ERR_NOMEM;
@@ -230,28 +324,29 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     }
 
     const unsigned n_ori = ctx->h_ctr[2];
-    ctx->h_ori.resize(n_ori);
-    ctx->h_off0.resize(n_ori);
+    if ((st = ctx->h_ori.ensure(n_ori)) != SIFT_OK) return st;
+    if ((st = ctx->h_off0.ensure(n_ori)) != SIFT_OK) return st;
     if (n_ori) {
-        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.data(), ctx->d_ori, n_ori * sizeof(sift_kp),
+        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.p, ctx->d_ori, n_ori * sizeof(sift_kp),
                                     hipMemcpyDeviceToHost, ctx->stream));
-        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.data(), ctx->d_off0, n_ori * sizeof(double),
+        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.p, ctx->d_off0, n_ori * sizeof(double),
                                     hipMemcpyDeviceToHost, ctx->stream));
     }
     if (out_desc_f32) {
-        ctx->h_df32.resize((size_t)n_ori * 128);
+        if ((st = ctx->h_df32.ensure((size_t)n_ori * 128)) != SIFT_OK) return st;
         if (n_ori)
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.data(), ctx->d_df32,
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.p, ctx->d_df32,
                                         (size_t)n_ori * 128 * sizeof(float),
                                         hipMemcpyDeviceToHost, ctx->stream));
     }
     SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const auto t_copy = clk::now();
 
     if (ctx->profiling) {
         for (const EventPair& e : ctx->pending) {
-            float ms = 0.f;
-            SIFT_HIP_TRY(hipEventElapsedTime(&ms, e.a, e.b));
-            ctx->prof_ms += ms;
+            float ems = 0.f;
+            SIFT_HIP_TRY(hipEventElapsedTime(&ems, e.a, e.b));
+            ctx->prof_ms += ems;
             ctx->prof_bytes += e.bytes;
             ctx->prof_launches += 1;
         }
@@ -259,11 +354,13 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     }
 
     // final size with glibc pow + clean_keypoints, in the g++-built layer
-    std::vector<unsigned> keep(n_ori);
-    const size_t n = host_finalize(p, ctx->h_ori.data(), ctx->h_off0.data(), n_ori, keep.data());
+    ctx->keep.resize(n_ori);
+    const size_t n = host_finalize(p, ctx->h_ori.p, ctx->h_off0.p, n_ori, ctx->keep.data());
+    const auto t_fin = clk::now();
+
     sift_kp* kps = (sift_kp*)std::malloc(std::max<size_t>(n, 1) * sizeof(sift_kp));
     if (!kps) return SIFT_ERR_NOMEM;
-    for (size_t i = 0; i < n; ++i) kps[i] = ctx->h_ori[keep[i]];
+    for (size_t i = 0; i < n; ++i) kps[i] = ctx->h_ori.p[ctx->keep[i]];
     float* df = nullptr;
     if (out_desc_f32) {
         df = (float*)std::malloc(std::max<size_t>(n, 1) * 128 * sizeof(float));
@@ -272,9 +369,15 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             return SIFT_ERR_NOMEM;
         }
         for (size_t i = 0; i < n; ++i)
-            std::memcpy(df + i * 128, ctx->h_df32.data() + (size_t)keep[i] * 128,
+            std::memcpy(df + i * 128, ctx->h_df32.p + (size_t)ctx->keep[i] * 128,
                         128 * sizeof(float));
     }
+    const auto t_out = clk::now();
+    ctx->t_host[0] = ms(t0, t_enq);
+    ctx->t_host[1] = ms(t_enq, t_wait);
+    ctx->t_host[2] = ms(t_wait, t_copy);
+    ctx->t_host[3] = ms(t_copy, t_fin);
+    ctx->t_host[4] = ms(t_fin, t_out);
     *out_kps = kps;
     *out_n = n;
     if (out_desc_f32) *out_desc_f32 = df;
@@ -326,10 +429,14 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ctx->d_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&ctx->h_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
-        hipMalloc(&ctx->d_pt, sizeof(PyrTable)) != hipSuccess) {
+        hipHostMalloc(&ctx->h_stage, sizeof(Stage)) != hipSuccess ||
+        hipMalloc(&ctx->d_stage, sizeof(Stage)) != hipSuccess ||
+        prepare_kernel_attributes() != hipSuccess) {
         sift_hip_destroy(ctx);
         return SIFT_ERR_HIP;
     }
+    ctx->d_pt = &ctx->d_stage->pt;
+    ctx->d_taps = ctx->d_stage->taps;
     *out = ctx;
     return SIFT_OK;
 }
@@ -339,10 +446,14 @@ int sift_hip_destroy(sift_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     void* bufs[] = {ctx->d_in, ctx->d_pyr, ctx->d_tmp, ctx->d_cand, ctx->d_raw,
-                    ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_pt};
+                    ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_stage};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->h_ctr) (void)hipHostFree(ctx->h_ctr);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    ctx->h_ori.release();
+    ctx->h_off0.release();
+    ctx->h_df32.release();
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -451,6 +562,13 @@ int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t*
         SIFT_HIP_TRY(hipMemcpyAsync(d_dst, ctx->d_ori, n * sizeof(sift_kp),
                                     hipMemcpyDeviceToDevice, ctx->stream));
     SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SIFT_OK;
+}
+
+int sift_hip_last_timing(sift_ctx* ctx, double* ms, int n) {
+    if (!ctx || !ms || n < 0) return SIFT_ERR_ARG;
+    if (!ctx->have_run) return SIFT_ERR_STATE;
+    for (int i = 0; i < n && i < 5; ++i) ms[i] = ctx->t_host[i];
     return SIFT_OK;
 }
 

@@ -30,18 +30,6 @@ bool make_taps(double sigma, BlurTaps* t) {
     return true;
 }
 
-bool kp_less(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator<, sift.hh:31-41
-    if (a.x != b.x) return a.x < b.x;
-    if (a.y != b.y) return a.y < b.y;
-    if (a.size != b.size) return a.size > b.size;
-    if (a.pori != b.pori) return a.pori < b.pori;
-    return a.octave > b.octave;
-}
-
-bool kp_equal(const sift_kp& a, const sift_kp& b) {  // Keypoint::operator==, sift.hh:25-27
-    return a.x == b.x && a.y == b.y && a.size == b.size && a.pori == b.pori;
-}
-
 }  // namespace
 
 int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* taps_init,
@@ -128,13 +116,36 @@ size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, un
         if (p->double_image_size) size /= 2;
         r.size = size;
     }
-    std::vector<unsigned> idx(n);
-    std::iota(idx.begin(), idx.end(), 0u);
-    std::sort(idx.begin(), idx.end(),
-              [&](unsigned a, unsigned b) { return kp_less(recs[a], recs[b]); });
-    size_t m = 0;
+    // sort a compact key array (40 B per record) rather than indices into
+    // the 168-byte records: same comparator, cache-friendly
+    struct Key {
+        double x, y, size, pori;
+        int octave;
+        unsigned idx;
+    };
+    std::vector<Key> keys(n);
     for (unsigned i = 0; i < n; ++i)
-        if (m == 0 || !kp_equal(recs[keep[m - 1]], recs[idx[i]])) keep[m++] = idx[i];
+        keys[i] = {recs[i].x, recs[i].y, recs[i].size, recs[i].pori, recs[i].octave, i};
+    // Keypoint::operator< (sift.hh:31-41)
+    std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) {
+        if (a.x != b.x) return a.x < b.x;
+        if (a.y != b.y) return a.y < b.y;
+        if (a.size != b.size) return a.size > b.size;
+        if (a.pori != b.pori) return a.pori < b.pori;
+        return a.octave > b.octave;
+    });
+    size_t m = 0;
+    for (unsigned i = 0; i < n; ++i) {
+        const Key& k = keys[i];
+        if (m > 0) {
+            // std::unique compares with the last kept element (Keypoint::
+            // operator==, sift.hh:25-27: x, y, size, pori)
+            const sift_kp& last = recs[keep[m - 1]];
+            if (last.x == k.x && last.y == k.y && last.size == k.size && last.pori == k.pori)
+                continue;
+        }
+        keep[m++] = k.idx;
+    }
     return m;
 }
 

@@ -11,14 +11,20 @@
 namespace sift_amd {
 
 int blur_rows_for(int W, int H, int R);
+hipError_t prepare_kernel_attributes();
 
 hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double* out,
                           int W0, int H0, hipStream_t s);
 hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurTaps& taps,
                        double* dec, int Wd, int Hd, double* tmp, hipStream_t s);
-hipError_t launch_extrema(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
-                          int window_size, int thr, sift_extremum* out, unsigned* counter,
-                          unsigned cap, hipStream_t s);
+hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
+                              const BlurTaps* d_taps, hipStream_t s);
+hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
+                                int thr, sift_extremum* out, unsigned* counter, unsigned cap,
+                                hipStream_t s);
+hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
+                              int window_size, int thr, sift_extremum* out, unsigned* counter,
+                              unsigned cap, hipStream_t s);
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P,
                          const sift_extremum* cand, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s);

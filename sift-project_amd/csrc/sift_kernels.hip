@@ -92,6 +92,7 @@ __global__ __launch_bounds__(256) void k_blur(const double* __restrict__ src,
                                               double* __restrict__ dst, int W, int H,
                                               int rows, BlurTaps taps,
                                               double* __restrict__ dec, int Wd, int Hd) {
+    constexpr int NW = 2 * R + 1;  // register window depth
     constexpr int SEG = 64 + 2 * R;
     __shared__ double sline[4][SEG];
     const int lane = threadIdx.x & 63;
@@ -111,45 +112,119 @@ __global__ __launch_bounds__(256) void k_blur(const double* __restrict__ src,
     for (int u = 0; u <= R; ++u) k[u] = taps.k[u];
     const double sw = taps.sum_w;
 
-    double win[2 * R + 1];
+    double win[NW];
 #pragma unroll
-    for (int q = 0; q <= 2 * R; ++q) win[q] = 0.0;
+    for (int q = 0; q < NW; ++q) win[q] = 0.0;
 
-    int yy = y_begin - R;
-    const int yy_end = y_end + R;
-    const double* srow = src + (size_t)clampi(yy, 0, H - 1) * W;
+    const int yy0 = y_begin - R, yy_end = y_end + R;
+    const double* srow = src + (size_t)clampi(yy0, 0, H - 1) * W;
     double a0 = srow[gx0];
     double a1 = has1 ? srow[gx1] : 0.0;
-    for (; yy < yy_end; ++yy) {
-        sl[lane] = a0;
-        if (has1) sl[64 + lane] = a1;
-        if (yy + 1 < yy_end) {  // prefetch the next source row
-            const double* nrow = src + (size_t)clampi(yy + 1, 0, H - 1) * W;
-            a0 = nrow[gx0];
-            if (has1) a1 = nrow[gx1];
-        }
-        wave_sync();
-        // horizontal pass (image.cpp:170-185)
-        double acc = sl[lane + R] * k[0];
+    // The row loop is unrolled by NW so that the window slot of every row is
+    // a compile-time constant: slot s of block yb holds horizontal-pass row
+    // yb+s, and no register moves are needed to slide the window.
+    for (int yb = yy0; yb < yy_end; yb += NW) {
 #pragma unroll
-        for (int u = 1; u <= R; ++u) acc += k[u] * (sl[lane + R + u] + sl[lane + R - u]);
-        const double t = acc / sw;
-        wave_sync();
+        for (int s = 0; s < NW; ++s) {
+            const int yy = yb + s;
+            if (yy < yy_end) {
+                sl[lane] = a0;
+                if (has1) sl[64 + lane] = a1;
+                if (yy + 1 < yy_end) {  // prefetch the next source row
+                    const double* nrow = src + (size_t)clampi(yy + 1, 0, H - 1) * W;
+                    a0 = nrow[gx0];
+                    if (has1) a1 = nrow[gx1];
+                }
+                wave_sync();
+                // horizontal pass (image.cpp:170-185)
+                double acc = sl[lane + R] * k[0];
 #pragma unroll
-        for (int q = 0; q < 2 * R; ++q) win[q] = win[q + 1];
-        win[2 * R] = t;
-        if (yy >= y_begin + R) {
-            // vertical pass for output row yy-R (image.cpp:193-208)
-            const int y = yy - R;
-            double o = win[R] * k[0];
+                for (int u = 1; u <= R; ++u) acc += k[u] * (sl[lane + R + u] + sl[lane + R - u]);
+                win[s] = acc / sw;
+                wave_sync();
+                if (yy >= y_begin + R) {
+                    // vertical pass for output row yy-R (image.cpp:193-208):
+                    // rows yy-2R..yy sit in slots s+1..s (mod NW)
+                    const int y = yy - R;
+                    double o = win[(s + R + 1) % NW] * k[0];
 #pragma unroll
-            for (int u = 1; u <= R; ++u) o += k[u] * (win[R + u] + win[R - u]);
-            o = o / sw;
-            if (x < W) {
-                dst[(size_t)y * W + x] = o;
-                if (DECIM && !(x & 1) && !(y & 1) && (x >> 1) < Wd && (y >> 1) < Hd)
-                    dec[(size_t)(y >> 1) * Wd + (x >> 1)] = o;
+                    for (int u = 1; u <= R; ++u)
+                        o += k[u] * (win[(s + NW - R + u) % NW] + win[(s + 2 * NW - R - u) % NW]);
+                    o = o / sw;
+                    if (x < W) {
+                        dst[(size_t)y * W + x] = o;
+                        if (DECIM && !(x & 1) && !(y & 1) && (x >> 1) < Wd && (y >> 1) < Hd)
+                            dec[(size_t)(y >> 1) * Wd + (x >> 1)] = o;
+                    }
+                }
             }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_octaves_lds: every remaining small octave (W*H <= kLdsOctavePx) in ONE
+// launch of ONE workgroup. A level and the horizontal-pass temporary both
+// live in LDS, so each level is two barrier-separated LDS sweeps instead of
+// a latency-bound launch; each finished level is streamed to its global
+// plane (needed later by extrema/orientation/descriptor), and the decimated
+// level `intervals` becomes the next octave's base in LDS. Same arithmetic
+// and order as k_blur (image.cpp:156-214), replicate borders by clamping.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
+                                                      int o_first, int o_last, int n_gauss,
+                                                      const BlurTaps* __restrict__ taps) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int dec_level = n_gauss - 3;
+    int W = pt->w[o_first], H = pt->h[o_first];
+    double* A = lds;                         // current level
+    double* T = lds + kLdsOctavePx;          // horizontal-pass temporary
+    double* D = lds + 2 * kLdsOctavePx;      // next octave's base
+    {
+        const double* g0 = pt->lvl[o_first][0];
+        for (int i = tid; i < W * H; i += nt) A[i] = g0[i];
+    }
+    __syncthreads();
+    for (int o = o_first; o <= o_last; ++o) {
+        W = pt->w[o];
+        H = pt->h[o];
+        const int N = W * H;
+        const bool has_next = o < o_last;
+        const int Wd = has_next ? pt->w[o + 1] : 0, Hd = has_next ? pt->h[o + 1] : 0;
+        for (int l = 1; l < n_gauss; ++l) {
+            const BlurTaps& t = taps[l];
+            const int R = t.R;
+            const double sw = t.sum_w;
+            for (int i = tid; i < N; i += nt) {
+                const int y = i / W, x = i - y * W;
+                const double* row = A + y * W;
+                double acc = row[x] * t.k[0];
+                for (int u = 1; u <= R; ++u)
+                    acc += t.k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
+                T[i] = acc / sw;
+            }
+            __syncthreads();
+            double* g = pt->lvl[o][l];
+            for (int i = tid; i < N; i += nt) {
+                const int y = i / W, x = i - y * W;
+                double acc = T[i] * t.k[0];
+                for (int u = 1; u <= R; ++u)
+                    acc += t.k[u] * (T[min(y + u, H - 1) * W + x] + T[max(y - u, 0) * W + x]);
+                const double v = acc / sw;
+                A[i] = v;
+                g[i] = v;
+                if (has_next && l == dec_level && !(x & 1) && !(y & 1) && (x >> 1) < Wd &&
+                    (y >> 1) < Hd) {
+                    D[(y >> 1) * Wd + (x >> 1)] = v;
+                    pt->lvl[o + 1][0][(y >> 1) * Wd + (x >> 1)] = v;
+                }
+            }
+            __syncthreads();
+        }
+        if (has_next) {
+            for (int i = tid; i < Wd * Hd; i += nt) A[i] = D[i];
+            __syncthreads();
         }
     }
 }
@@ -186,92 +261,80 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Extrema: detect_octave_extrema + is_extremum (sift.cpp:227-291) for
-// window_size 3 (border 1). A pixel is kept iff |D_z| > threshold (the int
-// threshold of sift.cpp:266,279) and it is a NON-strict maximum or minimum
-// of its 3x3x3 cube, i.e. v == max(cube) or v == min(cube) (v is in the
-// cube, so the centre comparison is vacuous, sift.cpp:241-246).
-//
-// One wavefront slides down a 64-column strip; per source row it stages the
-// DoG row segments (66 values per DoG level, computed as G_{l+1}-G_l on the
-// fly) in LDS, reduces them to 3-wide row max/min, and keeps three rows of
-// those in registers, so the 3x3 max/min of every level is 2+2 max ops per
-// row. Candidates are compacted per wave with a 64-bit ballot and one atomic.
+// Extrema: detect_octave_extrema + is_extremum (sift.cpp:227-291). A pixel is
+// kept iff |D_z| > threshold (the int threshold of sift.cpp:266,279) and it
+// is a NON-strict maximum or minimum of its (2b+1)^3 cube, i.e. v == max(cube)
+// or v == min(cube): v is itself in the cube, so the centre comparison is
+// vacuous (sift.cpp:241-246). DoG values are G_{l+1} - G_l computed on the fly.
 // ---------------------------------------------------------------------------
+// Tiled variant used for window_size 3: ONE launch covers every octave.
+// A 256-thread workgroup owns a 64x16 block of centre pixels of one octave;
+// it stages the (66x18)-pixel DoG halo tile of every DoG layer in LDS (six
+// Gaussian loads per staged pixel, all independent, so a tile costs one
+// memory round trip), then each thread takes one column x four centre rows:
+// per layer it forms 3-wide row max/min over six staged rows and the 3x3
+// max/min of its four centres in registers. Candidates are compacted with a
+// 64-bit ballot per (row, layer) and one atomic per wave.
 template <int NL>
-__global__ __launch_bounds__(256) void k_extrema3(const PyrTable* __restrict__ pt, int o,
-                                                  int thr, int rows,
-                                                  sift_extremum* __restrict__ out,
-                                                  unsigned* __restrict__ counter,
-                                                  unsigned cap) {
-    constexpr int ND = NL - 1;  // DoG layers
-    __shared__ double sd[4][ND][66];
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+__global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restrict__ pt,
+                                                       ExtremaGrid eg, int thr,
+                                                       sift_extremum* __restrict__ out,
+                                                       unsigned* __restrict__ counter,
+                                                       unsigned cap) {
+    constexpr int ND = NL - 1;
+    constexpr int TW = 64, TH = 16, SW = TW + 2, SH = TH + 2;
+    __shared__ double sd[ND][SH][SW];
+    const int tid = threadIdx.x, lane = tid & 63;
+    int o = 0;
+    while (o + 1 < eg.octaves && (int)blockIdx.x >= eg.first_tile[o + 1]) ++o;
+    const int tile = blockIdx.x - eg.first_tile[o];
+    const int tx = tile % eg.tiles_x[o], ty = tile / eg.tiles_x[o];
     const int W = pt->w[o], H = pt->h[o];
-    const int x0 = blockIdx.x * 64;
-    const int yc_begin = 1 + (blockIdx.y * 4 + wv) * rows;  // first centre row
-    if (yc_begin >= H - 1) return;
-    const int yc_end = min(yc_begin + rows, H - 1);
+    const int cx0 = 1 + tx * TW, cy0 = 1 + ty * TH;  // first centre of the tile
     const double* G[NL];
 #pragma unroll
     for (int l = 0; l < NL; ++l) G[l] = pt->lvl[o][l];
-    const int x = x0 + lane;
-    const int gxa = clampi(x0 - 1 + lane, 0, W - 1);
-    const bool hasb = lane < 2;
-    const int gxb = clampi(x0 + 63 + lane, 0, W - 1);
-    const bool xin = (x >= 1) && (x < W - 1);
-    const double dthr = (double)thr;
-
-    double rmax[ND][3], rmin[ND][3], cen[ND][2];
+    for (int i = tid; i < SH * SW; i += 256) {
+        const int r = i / SW, c = i - r * SW;
+        const size_t q = (size_t)clampi(cy0 - 1 + r, 0, H - 1) * W + clampi(cx0 - 1 + c, 0, W - 1);
+        double g[NL];
+#pragma unroll
+        for (int l = 0; l < NL; ++l) g[l] = G[l][q];
+#pragma unroll
+        for (int l = 0; l < ND; ++l) sd[l][r][c] = g[l + 1] - g[l];
+    }
+    __syncthreads();
+    const int c = lane;              // centre column in the tile
+    const int r0 = (tid >> 6) * 4;   // first of this thread's four centre rows
+    const int x = cx0 + c;
+    double cmax[ND][4], cmin[ND][4];
 #pragma unroll
     for (int l = 0; l < ND; ++l) {
-        rmax[l][0] = rmax[l][1] = rmax[l][2] = 0.0;
-        rmin[l][0] = rmin[l][1] = rmin[l][2] = 0.0;
-        cen[l][0] = cen[l][1] = 0.0;
+        double rmx[6], rmn[6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const double a = sd[l][r0 + r][c], b = sd[l][r0 + r][c + 1], d = sd[l][r0 + r][c + 2];
+            rmx[r] = fmax(fmax(a, b), d);
+            rmn[r] = fmin(fmin(a, b), d);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            cmax[l][k] = fmax(fmax(rmx[k], rmx[k + 1]), rmx[k + 2]);
+            cmin[l][k] = fmin(fmin(rmn[k], rmn[k + 1]), rmn[k + 2]);
+        }
     }
-    for (int yy = yc_begin - 1; yy <= yc_end; ++yy) {
-        const size_t ro = (size_t)yy * W;
-        double ga[NL], gb[NL];
+    const double dthr = (double)thr;
 #pragma unroll
-        for (int l = 0; l < NL; ++l) {
-            ga[l] = G[l][ro + gxa];
-            gb[l] = hasb ? G[l][ro + gxb] : 0.0;
-        }
-#pragma unroll
-        for (int l = 0; l < ND; ++l) {
-            sd[wv][l][lane] = ga[l + 1] - ga[l];
-            if (hasb) sd[wv][l][64 + lane] = gb[l + 1] - gb[l];
-        }
-        wave_sync();
-#pragma unroll
-        for (int l = 0; l < ND; ++l) {
-            const double a = sd[wv][l][lane], b = sd[wv][l][lane + 1], c = sd[wv][l][lane + 2];
-            rmax[l][0] = rmax[l][1];
-            rmax[l][1] = rmax[l][2];
-            rmax[l][2] = fmax(fmax(a, b), c);
-            rmin[l][0] = rmin[l][1];
-            rmin[l][1] = rmin[l][2];
-            rmin[l][2] = fmin(fmin(a, b), c);
-            cen[l][0] = cen[l][1];
-            cen[l][1] = b;  // D_l(yy, x)
-        }
-        wave_sync();
-        if (yy < yc_begin + 1) continue;
-        const int yc = yy - 1;  // centre row: its D values are cen[l][0]
-        double cmax[ND], cmin[ND];
-#pragma unroll
-        for (int l = 0; l < ND; ++l) {
-            cmax[l] = fmax(fmax(rmax[l][0], rmax[l][1]), rmax[l][2]);
-            cmin[l] = fmin(fmin(rmin[l][0], rmin[l][1]), rmin[l][2]);
-        }
+    for (int k = 0; k < 4; ++k) {
+        const int y = cy0 + r0 + k;
+        const bool in = x < W - 1 && y < H - 1;
 #pragma unroll
         for (int z = 1; z < ND - 1; ++z) {
-            const double v = cen[z][0];
+            const double v = sd[z][r0 + k + 1][c + 1];
             bool cand = false;
-            if (xin && fabs(v) > dthr) {
-                const double mx = fmax(fmax(cmax[z - 1], cmax[z]), cmax[z + 1]);
-                const double mn = fmin(fmin(cmin[z - 1], cmin[z]), cmin[z + 1]);
+            if (in && fabs(v) > dthr) {
+                const double mx = fmax(fmax(cmax[z - 1][k], cmax[z][k]), cmax[z + 1][k]);
+                const double mn = fmin(fmin(cmin[z - 1][k], cmin[z][k]), cmin[z + 1][k]);
                 cand = (v == mx) || (v == mn);
             }
             const unsigned long long m = __ballot(cand);
@@ -280,7 +343,7 @@ __global__ __launch_bounds__(256) void k_extrema3(const PyrTable* __restrict__ p
                 if (lane == 0) base = atomicAdd(counter, (unsigned)__popcll(m));
                 base = __shfl(base, 0);
                 const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-                if (cand && idx < cap) out[idx] = sift_extremum{x, yc, z, o};
+                if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, o};
             }
         }
     }
@@ -416,12 +479,15 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
 
 // ---------------------------------------------------------------------------
 // k_orient: compute_orientations (sift.cpp:447-533), one wavefront per
-// refined keypoint. Samples of the (2r+1)^2 window are evaluated 64-wide in
-// chunks and staged in LDS in the reference's scan order (i outer, j inner);
-// each lane then owns up to 4 bins and adds that chunk's values for its bins
-// sequentially, so every bin is summed in exactly the reference order
-// (sift.cpp:491). The in-place circular smoothing (sift.cpp:496-504) is a
-// Gauss-Seidel recurrence and runs sequentially on lane 0.
+// refined keypoint.
+//  * Samples are evaluated 64-wide in chunks of whole window columns, lanes
+//    running along x so the four gradient loads coalesce, and staged in LDS
+//    in the reference's scan order (i = x offset outer, j = y offset inner).
+//  * Each lane owns up to four bins and adds the staged values of its bins
+//    sequentially, eight per step from vector LDS reads, so every bin is
+//    summed in exactly the reference order (sift.cpp:491).
+//  * The in-place circular smoothing (sift.cpp:496-504) is a Gauss-Seidel
+//    recurrence and runs on lane 0 with the running value in a register.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt, DevParams P,
                                                 const RawKp* __restrict__ raw,
@@ -430,9 +496,9 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
                                                 double* __restrict__ out_off0,
                                                 unsigned* __restrict__ n_out,
                                                 unsigned cap_out) {
-    constexpr int CH = 512;
-    __shared__ double sval[4][CH];
-    __shared__ short sbin[4][CH];
+    constexpr int CH = 640;  // staged samples per chunk (multiple of 8)
+    __shared__ __attribute__((aligned(16))) double sval[4][CH];
+    __shared__ __attribute__((aligned(16))) short sbin[4][CH];
     __shared__ double shist[4][kMaxBins];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -452,37 +518,62 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
         const double* img = pt->lvl[o][kp.layer];
         const int W = pt->w[o], H = pt->h[o];
         const int side = 2 * radius + 1;
-        const int ns = side * side;
+        // chunk = ncol whole columns (i values); a lane covers (di, dj)
+        const int ncol = max(1, min(CH / side, 64));
+        const int lrows = 64 / ncol;
+        const int di = lane % ncol, dj = lane / ncol;
+        const bool lane_on = dj < lrows;
         double hb[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int base = 0; base < ns; base += CH) {
-            const int cnt = min(CH, ns - base);
-            for (int s = lane; s < cnt; s += 64) {
-                const int si = base + s;
-                const int i = si / side - radius;
-                const int j = si % side - radius;
-                short bin = -1;
-                double val = 0.0;
-                if (!(x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H)) {
-                    const size_t r0 = (size_t)(y + j) * W;
-                    const double dx = img[r0 + x + i + 1] - img[r0 + x + i - 1];
-                    const double dy = img[r0 - W + x + i] - img[r0 + W + x + i];
-                    const double mag = sqrt(dx * dx + dy * dy);
-                    const double ang = atan2(dy, dx);
-                    const double wgt = exp(-(i * i + j * j) / denom);
-                    int hidx = (int)round(nb * (ang + kPi) / kTwoPi);
-                    hidx = (hidx < nb) ? hidx : 0;
-                    bin = (short)hidx;
-                    val = wgt * mag;
+        for (int ic = 0; ic < side; ic += ncol) {
+            const int nci = min(ncol, side - ic);
+            const int cnt = nci * side;
+            for (int jq = dj; lane_on && jq < side; jq += lrows) {
+                const int iq = di;
+                if (iq < nci) {
+                    const int i = ic + iq - radius, j = jq - radius;
+                    short bin = -1;
+                    double val = 0.0;
+                    if (!(x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H)) {
+                        const size_t r0 = (size_t)(y + j) * W;
+                        const double dx = img[r0 + x + i + 1] - img[r0 + x + i - 1];
+                        const double dy = img[r0 - W + x + i] - img[r0 + W + x + i];
+                        const double mag = sqrt(dx * dx + dy * dy);
+                        const double ang = atan2(dy, dx);
+                        const double wgt = exp(-(i * i + j * j) / denom);
+                        int hidx = (int)round(nb * (ang + kPi) / kTwoPi);
+                        hidx = (hidx < nb) ? hidx : 0;
+                        bin = (short)hidx;
+                        val = wgt * mag;
+                    }
+                    const int t = iq * side + jq;  // reference order within the chunk
+                    sval[wv][t] = val;
+                    sbin[wv][t] = bin;
                 }
-                sval[wv][s] = val;
-                sbin[wv][s] = bin;
             }
+            const int cnt8 = (cnt + 7) & ~7;
+            for (int t = cnt + lane; t < cnt8; t += 64) sbin[wv][t] = -1;
             wave_sync();
-            for (int t = 0; t < cnt; ++t) {
-                const int bsel = sbin[wv][t];
-                const double v = sval[wv][t];
-                for (int q = 0; q < nbq; ++q)
-                    if (bsel == lane + 64 * q) hb[q] += v;
+            for (int t = 0; t < cnt8; t += 8) {
+                const short4 b0 = *reinterpret_cast<const short4*>(&sbin[wv][t]);
+                const short4 b1 = *reinterpret_cast<const short4*>(&sbin[wv][t + 4]);
+                const double2 v0 = *reinterpret_cast<const double2*>(&sval[wv][t]);
+                const double2 v1 = *reinterpret_cast<const double2*>(&sval[wv][t + 2]);
+                const double2 v2 = *reinterpret_cast<const double2*>(&sval[wv][t + 4]);
+                const double2 v3 = *reinterpret_cast<const double2*>(&sval[wv][t + 6]);
+                const short bs[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                const double vs[8] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    // adding +0.0 never changes a non-negative bin sum
+                    hb[0] += (bs[e] == lane) ? vs[e] : 0.0;
+                    if (nbq > 1) {
+                        hb[1] += (bs[e] == lane + 64) ? vs[e] : 0.0;
+                        if (nbq > 2) {
+                            hb[2] += (bs[e] == lane + 128) ? vs[e] : 0.0;
+                            hb[3] += (bs[e] == lane + 192) ? vs[e] : 0.0;
+                        }
+                    }
+                }
             }
             wave_sync();
         }
@@ -491,10 +582,21 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
         wave_sync();
         if (lane == 0) {
             double* hs = shist[wv];
-            for (int it = 0; it < kSmoothIters; ++it)
-                for (int i = 0; i < nb; ++i)
-                    hs[i] = 0.25 * hs[(i - 1 + nb) % nb] + 0.5 * hs[i] +
-                            0.25 * hs[(i + 1) % nb];
+            for (int it = 0; it < kSmoothIters; ++it) {
+                double prev = hs[nb - 1];  // h[i-1] for i = 0: not yet updated
+                const double h0_old = hs[0];
+                double first_new = 0.0;
+                for (int i = 0; i < nb; ++i) {
+                    const double h1 = hs[i];
+                    // h[i+1]: old value, except for i = nb-1 where it is the
+                    // already-updated h[0] (and h[0] itself when nb == 1)
+                    const double h2 = (i + 1 < nb) ? hs[i + 1] : (i == 0 ? h0_old : first_new);
+                    const double v = 0.25 * prev + 0.5 * h1 + 0.25 * h2;
+                    hs[i] = v;
+                    prev = v;
+                    if (i == 0) first_new = v;
+                }
+            }
         }
         wave_sync();
         double mx = 0.0;  // histogram entries are >= 0
@@ -507,9 +609,9 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
             bool peak = false;
             double ori = 0.0;
             if (i < nb) {
-                const double h0 = shist[wv][(i - 1 + nb) % nb];
+                const double h0 = shist[wv][i == 0 ? nb - 1 : i - 1];
                 const double h1 = shist[wv][i];
-                const double h2 = shist[wv][(i + 1) % nb];
+                const double h2 = shist[wv][i + 1 == nb ? 0 : i + 1];
                 if (h1 > h0 && h1 > h2 && h1 > (P.peak_ratio * mx)) {
                     double fi = i + 0.5 * (h0 - h2) / (h0 - 2 * h1 + h2);
                     fi = fmod(fi + nb, (double)nb);
@@ -549,19 +651,28 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
 
 // ---------------------------------------------------------------------------
 // k_descriptor: compute_descriptors + update_histogram + convert_hist_to_desc
-// (sift.cpp:541-682), one wavefront per oriented keypoint. Window samples are
-// strided over the lanes; each accepted sample's trilinear split adds into a
-// per-wave 4x4x8 f64 histogram in LDS (ds_add_f64; one wave per histogram,
-// so the result is reproducible run to run). The two normalisation sums run
-// sequentially on lane 0 in index order (sift.cpp:583-596).
+// (sift.cpp:541-682), one wavefront per oriented keypoint.
+//  * Phase A walks the (2r+1)^2 window 64 samples at a time (lanes along x),
+//    applies the rotated-box and image-border tests (sift.cpp:651-656) and
+//    compacts the accepted ~half into a per-wave LDS ring;
+//  * phase B drains the ring 64 at a time through the expensive part
+//    (gradient, atan2, exp weight, trilinear split), so no lane idles on a
+//    rejected sample. The two fmods of sift.cpp:667 reduce exactly to
+//    compare-and-subtract (|angle| < 2*2pi; fmod results are exact).
+//  * Histogram adds go to a per-wave 4x4x8 f64 histogram in LDS (ds_add_f64;
+//    one wave per histogram, so results are reproducible run to run). The
+//    two normalisation sums run sequentially on lane 0 in index order.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__ pt,
                                                     DevParams P, sift_kp* __restrict__ recs,
                                                     const unsigned* __restrict__ n_p,
                                                     unsigned cap,
                                                     float* __restrict__ desc_f32) {
+    constexpr int RING = 256;  // power of two
     __shared__ double sh[4][128];
     __shared__ double sinv[4];
+    __shared__ double qrr[4][RING], qcr[4][RING];
+    __shared__ int qxy[4][RING];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const unsigned n = min(*n_p, cap);
@@ -589,45 +700,92 @@ __global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__
         wave_sync();
         const int side = 2 * radius + 1;
         const int ns = side * side;
-        for (int s = lane; s < ns; s += 64) {
-            const int row = s / side - radius;
-            const int col = s % side - radius;
-            const double row_rot = (col * sa + row * ca) / hw;
-            const double col_rot = (col * ca - row * sa) / hw;
-            const double rb = row_rot + kDescW / 2 - 0.5;
-            const double cb = col_rot + kDescW / 2 - 0.5;
-            if (!(rb > -1.0 && rb < kDescW && cb > -1.0 && cb < kDescW)) continue;
-            const int ny = row + y, nx = col + x;
-            if (!(nx > 0 && nx < (W - 1) && ny > 0 && ny < (H - 1))) continue;
-            const size_t r0 = (size_t)ny * W;
-            const double dx = img[r0 + nx + 1] - img[r0 + nx - 1];
-            const double dy = img[r0 - W + nx] - img[r0 + W + nx];
-            const double mag = sqrt(dx * dx + dy * dy);
-            double ang = atan2(dy, dx);
-            ang -= pori;
-            ang = fmod(fmod(ang, kTwoPi) + kTwoPi, kTwoPi);
-            const double ob = ang * bins_per_rad;
-            const double wgt = exp(-(row_rot * row_rot + col_rot * col_rot) / denom);
-            const double m = mag * wgt;
-            const int br = (int)floor(rb), bc = (int)floor(cb), bo = (int)floor(ob);
-            const double fr = rb - br, fc = cb - bc, fo = ob - bo;
+        int s0 = 0;         // next window sample to classify
+        unsigned head = 0;  // ring read position
+        unsigned tail = 0;  // ring write position
+        while (true) {
+            const unsigned queued = tail - head;
+            if (queued < 64 && s0 < ns) {
+                // ---- phase A: classify 64 samples, compact the accepted ones
+                const int s = s0 + lane;
+                bool acc = false;
+                double row_rot = 0.0, col_rot = 0.0;
+                int nx = 0, ny = 0;
+                if (s < ns) {
+                    const int row = s / side - radius;
+                    const int col = s % side - radius;
+                    row_rot = (col * sa + row * ca) / hw;
+                    col_rot = (col * ca - row * sa) / hw;
+                    const double rb = row_rot + kDescW / 2 - 0.5;
+                    const double cb = col_rot + kDescW / 2 - 0.5;
+                    ny = row + y;
+                    nx = col + x;
+                    acc = rb > -1.0 && rb < kDescW && cb > -1.0 && cb < kDescW && nx > 0 &&
+                          nx < (W - 1) && ny > 0 && ny < (H - 1);
+                }
+                const unsigned long long m = __ballot(acc);
+                if (acc) {
+                    const unsigned slot =
+                        (tail + (unsigned)__popcll(m & ((1ull << lane) - 1ull))) & (RING - 1);
+                    qrr[wv][slot] = row_rot;
+                    qcr[wv][slot] = col_rot;
+                    qxy[wv][slot] = (ny << 16) | nx;
+                }
+                tail += (unsigned)__popcll(m);
+                s0 += 64;
+                wave_sync();
+                continue;
+            }
+            if (queued == 0) break;
+            // ---- phase B: drain up to 64 accepted samples
+            const unsigned take = queued < 64 ? queued : 64;
+            if ((unsigned)lane < take) {
+                const unsigned slot = (head + lane) & (RING - 1);
+                const double row_rot = qrr[wv][slot], col_rot = qcr[wv][slot];
+                const int pxy = qxy[wv][slot];
+                const int nx = pxy & 0xFFFF, ny = pxy >> 16;
+                const double rb = row_rot + kDescW / 2 - 0.5;
+                const double cb = col_rot + kDescW / 2 - 0.5;
+                const size_t r0 = (size_t)ny * W;
+                const double dx = img[r0 + nx + 1] - img[r0 + nx - 1];
+                const double dy = img[r0 - W + nx] - img[r0 + W + nx];
+                const double mag = sqrt(dx * dx + dy * dy);
+                double ang = atan2(dy, dx);
+                ang -= pori;
+                // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi:
+                // fmod(a, M) = a - trunc(a/M) M is exact and representable,
+                // so one compare-and-subtract reproduces it bit for bit.
+                if (ang >= kTwoPi) ang -= kTwoPi;
+                else if (ang <= -kTwoPi) ang += kTwoPi;
+                ang += kTwoPi;  // rounded, as in the reference
+                if (ang >= kTwoPi) ang -= kTwoPi;
+                if (ang >= kTwoPi) ang -= kTwoPi;
+                const double ob = ang * bins_per_rad;
+                const double wgt = exp(-(row_rot * row_rot + col_rot * col_rot) / denom);
+                const double m = mag * wgt;
+                const int br = (int)floor(rb), bc = (int)floor(cb), bo = (int)floor(ob);
+                const double fr = rb - br, fc = cb - bc, fo = ob - bo;
 #pragma unroll
-            for (int r = 0; r <= 1; ++r) {
-                const int ri = br + r;
-                if (ri < 0 || ri >= kDescW) continue;
-                const double vr = m * ((r == 0) ? 1.0 - fr : fr);
+                for (int r = 0; r <= 1; ++r) {
+                    const int ri = br + r;
+                    if (ri < 0 || ri >= kDescW) continue;
+                    const double vr = m * ((r == 0) ? 1.0 - fr : fr);
 #pragma unroll
-                for (int c = 0; c <= 1; ++c) {
-                    const int ci = bc + c;
-                    if (ci < 0 || ci >= kDescW) continue;
-                    const double vc = vr * ((c == 0) ? 1.0 - fc : fc);
+                    for (int c = 0; c <= 1; ++c) {
+                        const int ci = bc + c;
+                        if (ci < 0 || ci >= kDescW) continue;
+                        const double vc = vr * ((c == 0) ? 1.0 - fc : fc);
 #pragma unroll
-                    for (int q = 0; q <= 1; ++q) {
-                        const int oi = (bo + q) % kDescBins;
-                        atomicAdd(&sh[wv][ri * 32 + ci * 8 + oi], vc * ((q == 0) ? 1.0 - fo : fo));
+                        for (int q = 0; q <= 1; ++q) {
+                            const int oi = (bo + q) % kDescBins;
+                            atomicAdd(&sh[wv][ri * 32 + ci * 8 + oi],
+                                      vc * ((q == 0) ? 1.0 - fo : fo));
+                        }
                     }
                 }
             }
+            head += take;
+            wave_sync();
         }
         wave_sync();
         if (lane == 0) {
@@ -690,20 +848,20 @@ struct BlurTable {
 template <int... Rs>
 constexpr BlurFn BlurTable<Rs...>::fns[sizeof...(Rs)];
 
-using BlurAll = BlurTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18,
-                          19, 20, 21, 22, 23, 24>;
-static_assert(kMaxTemplR == 24, "BlurAll must cover 1..kMaxTemplR");
+using BlurAll = BlurTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
+static_assert(kMaxTemplR == 16, "BlurAll must cover 1..kMaxTemplR");
 
 int blur_rows_for(int W, int H, int R) {
-    // enough wavefronts to fill 256 CUs several times over, but strips tall
-    // enough that the 2R-row priming stays a modest fraction
+    // Strip height trades the 2R-row priming of every strip against the
+    // number of wavefronts in flight; measured on MI355X
+    // (tools/blur_variants.hip): ~4096 waves is the sweet spot for 4K
+    // levels, small levels are latency-bound and want 4-8 row strips.
     const int nsx = (W + 63) / 64;
-    long want = 4096;
-    int rows = (int)((long)H * nsx / want);
-    const int min_rows = 2 * R + 12 > 32 ? 2 * R + 12 : 32;
+    int rows = (int)(((long)H * nsx + 4095) / 4096);
+    const int min_rows = R >= 8 ? 12 : 4;
     if (rows < min_rows) rows = min_rows;
+    if (rows > 32) rows = 32;
     if (rows > H) rows = H;
-    if (rows < 1) rows = 1;
     return rows;
 }
 
@@ -722,6 +880,20 @@ hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurT
     return hipGetLastError();
 }
 
+hipError_t prepare_kernel_attributes() {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_octaves_lds),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kLdsOctaveBytes);
+}
+
+hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
+                              const BlurTaps* d_taps, hipStream_t s) {
+    const size_t lds = kLdsOctaveBytes;
+    hipLaunchKernelGGL(k_octaves_lds, dim3(1), dim3(1024), lds, s, d_pt, o_first, o_last,
+                       n_gauss, d_taps);
+    return hipGetLastError();
+}
+
 hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double* out,
                           int W0, int H0, hipStream_t s) {
     dim3 grid((W0 + 255) / 256, H0);
@@ -729,36 +901,36 @@ hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double
     return hipGetLastError();
 }
 
-hipError_t launch_extrema(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
-                          int window_size, int thr, sift_extremum* out, unsigned* counter,
-                          unsigned cap, hipStream_t s) {
-    const int b = window_size / 2;
-    if (b == 1) {
-        const int nsx = (W + 63) / 64;
-        int rows = (int)((long)(H - 2) * nsx / 4096);
-        if (rows < 16) rows = 16;
-        const int nstrips = (H - 2 + rows - 1) / rows;
-        dim3 grid(nsx, (nstrips + 3) / 4);
-        if (grid.y == 0) return hipSuccess;
-        switch (n_gauss) {
-#define SIFT_EXT_CASE(NL)                                                              \
-    case NL:                                                                           \
-        hipLaunchKernelGGL((k_extrema3<NL>), grid, dim3(256), 0, s, d_pt, o, thr, rows, \
-                           out, counter, cap);                                         \
+hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
+                                int thr, sift_extremum* out, unsigned* counter, unsigned cap,
+                                hipStream_t s) {
+    const int blocks = eg.first_tile[eg.octaves];
+    if (blocks == 0) return hipSuccess;
+    switch (n_gauss) {
+#define SIFT_EXT_CASE(NL)                                                                 \
+    case NL:                                                                              \
+        hipLaunchKernelGGL((k_extrema_tiles<NL>), dim3(blocks), dim3(256), 0, s, d_pt, eg, \
+                           thr, out, counter, cap);                                       \
         return hipGetLastError();
-            SIFT_EXT_CASE(4)
-            SIFT_EXT_CASE(5)
-            SIFT_EXT_CASE(6)
-            SIFT_EXT_CASE(7)
-            SIFT_EXT_CASE(8)
-            SIFT_EXT_CASE(9)
-            SIFT_EXT_CASE(10)
-            SIFT_EXT_CASE(11)
+        SIFT_EXT_CASE(4)
+        SIFT_EXT_CASE(5)
+        SIFT_EXT_CASE(6)
+        SIFT_EXT_CASE(7)
+        SIFT_EXT_CASE(8)
+        SIFT_EXT_CASE(9)
+        SIFT_EXT_CASE(10)
+        SIFT_EXT_CASE(11)
+        SIFT_EXT_CASE(12)
 #undef SIFT_EXT_CASE
-            default:
-                break;
-        }
+        default:
+            return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
+                              int window_size, int thr, sift_extremum* out, unsigned* counter,
+                              unsigned cap, hipStream_t s) {
+    const int b = window_size / 2;
     dim3 grid((W + 255) / 256, H);
     hipLaunchKernelGGL(k_extrema_any, grid, dim3(256), 0, s, d_pt, o, thr, b, n_gauss - 1, out,
                        counter, cap);

@@ -4,6 +4,7 @@
 // the reference (g++), which matters for glibc-exact host math.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 
 #include "../../include/sift_hip.h"
@@ -21,9 +22,14 @@ constexpr double kIntFactor = 512.0;  // INT_DESCR_FCTR
 
 constexpr int kMaxOctaves = 16;   // floor(log2(min/3)) < 16 for any int image
 constexpr int kMaxLevels = 12;    // intervals + 3 with intervals <= 9
-constexpr int kMaxTemplR = 24;    // widest register-window blur kernel
+constexpr int kMaxTemplR = 16;    // widest register-window blur kernel (the
+                                  // NW-unrolled body stops unrolling past 16)
 constexpr int kMaxTaps = 64;      // generic path: kernels up to 64 taps
 constexpr int kMaxBins = 256;     // orientation bins supported
+// octaves of at most this many pixels run LDS-resident: level + temporary +
+// quarter-size next base = 2.25 * 9088 * 8 B = 163,584 B of the 163,840 B LDS
+constexpr int kLdsOctavePx = 9088;
+constexpr size_t kLdsOctaveBytes = (2 * (size_t)kLdsOctavePx + kLdsOctavePx / 4) * sizeof(double);
 
 // Half kernel of apply_gaussian_blur_fast (image.cpp:226-235) plus its
 // normalising sum (image.cpp:171-185), computed on the host with glibc.
@@ -39,6 +45,15 @@ struct PyrTable {
     double* lvl[kMaxOctaves][kMaxLevels];
     int w[kMaxOctaves];
     int h[kMaxOctaves];
+};
+
+// Flattened tile grid of the all-octave extrema launch: octave o owns blocks
+// [first_tile[o], first_tile[o+1]), tiles_x[o] tiles of 64 centre columns per
+// row of 16 centre rows.
+struct ExtremaGrid {
+    int octaves;
+    int tiles_x[kMaxOctaves];
+    int first_tile[kMaxOctaves + 1];
 };
 
 // Scalar parameters of detect_keypoints_and_descriptors as the kernels need

@@ -61,6 +61,7 @@ EXPORTS = (
     "sift_hip_copy_level",
     "sift_hip_copy_extrema",
     "sift_hip_copy_records_device",
+    "sift_hip_last_timing",
     "sift_hip_stream",
     "sift_hip_set_profiling",
     "sift_hip_blur_profile",
@@ -154,6 +155,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sift_hip_copy_level.argtypes = [vp, i, i, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
     lib.sift_hip_copy_extrema.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     lib.sift_hip_copy_records_device.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    lib.sift_hip_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i]
     lib.sift_hip_stream.argtypes = [vp]
     lib.sift_hip_stream.restype = vp
     lib.sift_hip_set_profiling.argtypes = [vp, i]
@@ -215,8 +217,8 @@ class Context:
     def _finish(self, kp_ptr, n, df_ptr, want_f32):
         n = n.value
         try:
-            kps = np.frombuffer(ctypes.string_at(kp_ptr.value, n * 168), dtype=KP_DTYPE).copy() \
-                if n else np.zeros(0, dtype=KP_DTYPE)
+            kps = np.ctypeslib.as_array((ctypes.c_uint8 * (n * 168)).from_address(kp_ptr.value)) \
+                .view(KP_DTYPE).copy() if n else np.zeros(0, dtype=KP_DTYPE)
             df = None
             if want_f32:
                 df = np.frombuffer(ctypes.string_at(df_ptr.value, n * 512), dtype="<f4") \
@@ -281,6 +283,12 @@ class Context:
         n = ctypes.c_size_t()
         _check(self.lib.sift_hip_copy_records_device(self._ctx, None, 0, ctypes.byref(n)))
         return n.value
+
+    def host_timing(self) -> dict:
+        """Host-side phase wall times (ms) of the last detect."""
+        t = (ctypes.c_double * 5)()
+        _check(self.lib.sift_hip_last_timing(self._ctx, t, 5))
+        return dict(zip(("enqueue", "wait_device", "download", "finalize", "output"), list(t)))
 
     @property
     def stream(self) -> int:

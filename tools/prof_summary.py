@@ -1,0 +1,38 @@
+"""Summarise a rocprofv3 kernel trace (CSV) per kernel and for one image.
+
+usage: python tools/prof_summary.py <run_kernel_trace.csv> [--images N]
+"""
+import collections
+import csv
+import sys
+
+
+def main(path, n_images=None):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    tot = collections.defaultdict(float)
+    cnt = collections.Counter()
+    for r in rows:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+        tot[r["Kernel_Name"]] += d
+        cnt[r["Kernel_Name"]] += 1
+    starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_prepare")]
+    n_img = n_images or len(starts)
+    print(f"{'kernel':40s} {'calls':>6s} {'total us':>10s} {'avg us':>9s} {'us/image':>9s}")
+    for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
+        print(f"{k[:40]:40s} {cnt[k]:6d} {v:10.1f} {v / cnt[k]:9.2f} {v / n_img:9.1f}")
+    if len(starts) >= 2:
+        a, b = starts[-2], starts[-1]
+        seg = rows[a:b]
+        t0 = int(seg[0]["Start_Timestamp"])
+        t1 = int(rows[b]["Start_Timestamp"])
+        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg) / 1000.0
+        print(f"\none image (second to last): {len(seg)} dispatches, kernel busy {busy:.1f} us, "
+              f"span to next image {(t1 - t0) / 1000.0:.1f} us")
+        for r in seg:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+            print(f"  {r['Kernel_Name'][:30]:30s} {d:8.1f} us  grid {r['Grid_Size_X']}x{r['Grid_Size_Y']}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
