@@ -27,6 +27,10 @@ using namespace sift_amd;
 
 namespace {
 
+// device counter block: [0..3] live counters (candidates, refined, oriented),
+// [4..7] batch-0 begin (zeros), [8..11] batch-1 begin (snapshot)
+constexpr int kCtrWords = 12;
+
 template <class T>
 struct Pinned {  // grow-only pinned host buffer (fast async D2H, no staging)
     T* p = nullptr;
@@ -62,7 +66,9 @@ struct EventPair {
 
 struct sift_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // A: pyramid
+    hipStream_t stream2 = nullptr;  // B: extrema, refine, orientation, descriptor
+    std::vector<hipEvent_t> sync_ev;
 
     double* d_in = nullptr;
     size_t in_cap = 0;  // elements
@@ -105,6 +111,7 @@ struct sift_ctx {
     Pinned<double> h_off0;
     Pinned<float> h_df32;
     std::vector<unsigned> keep;
+    FinalizeWorkspace fin_ws;
 
     // host-side phase wall times of the last detect (ms): enqueue, wait for
     // the device pipeline, records download, finalize (size + sort/unique),
@@ -150,26 +157,51 @@ hipEvent_t next_event(sift_ctx* ctx) {
     return ctx->ev_pool[ctx->ev_used++];
 }
 
+// Profiling events for one pyramid launch: timestamps recorded by the
+// dispatch packet itself (hipExtLaunchKernel), so timing adds no gaps.
+int prof_events(sift_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1, double bytes) {
+    *e0 = *e1 = nullptr;
+    if (!ctx->profiling) return SIFT_OK;
+    *e0 = next_event(ctx);
+    *e1 = next_event(ctx);
+    if (!*e0 || !*e1) return SIFT_ERR_HIP;
+    ctx->pending.push_back({*e0, *e1, bytes});
+    return SIFT_OK;
+}
+
 int blur_launch(sift_ctx* ctx, const double* src, double* dst, int W, int H,
                 const BlurTaps& t, double* dec, int Wd, int Hd) {
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (ctx->profiling) {
-        ea = next_event(ctx);
-        eb = next_event(ctx);
-        if (!ea || !eb) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(ea, ctx->stream));
-    }
     if (t.R > kMaxTemplR || t.R < 1) {
         if (ensure(&ctx->d_tmp, &ctx->tmp_cap, (size_t)W * H) != SIFT_OK) return SIFT_ERR_NOMEM;
     }
-    SIFT_HIP_TRY(launch_blur(src, dst, W, H, t, dec, Wd, Hd, ctx->d_tmp, ctx->stream));
-    if (ctx->profiling) {
-        SIFT_HIP_TRY(hipEventRecord(eb, ctx->stream));
-        double bytes = 16.0 * (double)W * (double)H;
-        if (dec) bytes += 8.0 * (double)Wd * (double)Hd;
-        ctx->pending.push_back({ea, eb, bytes});
-    }
+    hipEvent_t e0, e1;
+    const double bytes = 16.0 * (double)W * (double)H + (dec ? 8.0 * (double)Wd * Hd : 0.0);
+    if (prof_events(ctx, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
+    SIFT_HIP_TRY(launch_blur(src, dst, W, H, t, dec, Wd, Hd, ctx->d_tmp, ctx->stream, e0, e1));
     return SIFT_OK;
+}
+
+hipEvent_t sync_event(sift_ctx* ctx, int i) {  // untimed cross-stream events
+    while ((int)ctx->sync_ev.size() <= i) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        ctx->sync_ev.push_back(e);
+    }
+    return ctx->sync_ev[i];
+}
+
+ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end) {
+    ExtremaGrid eg;
+    std::memset(&eg, 0, sizeof eg);
+    for (int o = o_begin; o < o_end; ++o) {
+        const int i = eg.n++;
+        const int tx = g.W[o] > 2 ? (g.W[o] - 2 + 63) / 64 : 0;
+        const int ty = g.H[o] > 2 ? (g.H[o] - 2 + 15) / 16 : 0;
+        eg.oct[i] = o;
+        eg.tiles_x[i] = tx > 0 ? tx : 1;
+        eg.first_tile[i + 1] = eg.first_tile[i] + tx * ty;
+    }
+    return eg;
 }
 
 int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
@@ -216,20 +248,41 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         (st = ensure_t(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
         return st;
 
+    // Two streams: A (ctx->stream) builds the pyramid; B (ctx->stream2) runs
+    // the extrema of every octave as soon as that octave is complete (event
+    // per octave), then the small octaves' extrema after the LDS-resident
+    // kernel, then refine -> orientation -> descriptor. The octave-0 extrema
+    // overlap the octave-1..k blurs, and the single-CU small-octave kernel
+    // overlaps the big octaves' extrema.
+    hipStream_t sA = ctx->stream, sB = ctx->stream2;
+    int ev_i = 0;
+
     // ---- Gaussian pyramid (compute_initial_image + compute_gaussian_images)
     const int W0 = g.W[0], H0 = g.H[0];
     double* G00 = ctx->h_pt.lvl[0][0];
-    const double* base_src = d_img;
-    if (c != 1 || p->double_image_size) {
-        // gray (+ bilinear x2) into level 1's storage; level 1 is written by
-        // the first octave blur, after G[0][0] has been produced from it
-        double* scratch = ctx->h_pt.lvl[0][1];
-        SIFT_HIP_TRY(launch_prepare(d_img, w, h, c, p->double_image_size ? 1 : 0, scratch,
-                                    W0, H0, ctx->stream));
-        base_src = scratch;
+    {
+        hipEvent_t e0, e1;
+        if (prof_events(ctx, &e0, &e1, 16.0 * (double)W0 * H0) != SIFT_OK) return SIFT_ERR_HIP;
+        hipError_t err = hipSuccess;
+        const bool fused = launch_blur_initial_fused(d_img, w, h, c, p->double_image_size ? 1 : 0,
+                                                     G00, W0, H0, taps_init, sA, e0, e1, &err);
+        if (fused) {
+            SIFT_HIP_TRY(err);
+        } else {
+            if (ctx->profiling) ctx->pending.pop_back();
+            const double* base_src = d_img;
+            if (c != 1 || p->double_image_size) {
+                // gray (+ bilinear x2) into level 1's storage; level 1 is
+                // written by the first octave blur, after G[0][0] exists
+                double* scratch = ctx->h_pt.lvl[0][1];
+                SIFT_HIP_TRY(launch_prepare(d_img, w, h, c, p->double_image_size ? 1 : 0,
+                                            scratch, W0, H0, sA));
+                base_src = scratch;
+            }
+            if ((st = blur_launch(ctx, base_src, G00, W0, H0, taps_init, nullptr, 0, 0)) != SIFT_OK)
+                return st;
+        }
     }
-    if ((st = blur_launch(ctx, base_src, G00, W0, H0, taps_init, nullptr, 0, 0)) != SIFT_OK)
-        return st;
     const int dec_level = g.n_gauss - 3;  // = intervals (sift.cpp:195-196)
     // octaves from o_small on are small enough to run LDS-resident in one
     // launch (k_octaves_lds); the larger ones get one k_blur launch per level
@@ -239,6 +292,22 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             o_small = o;
             break;
         }
+    const bool tiles = p->window_size / 2 == 1;
+    SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sB));
+    // refine -> orientation -> descriptor over the records appended since
+    // the counter snapshot `begin` (batch ranges, see launch_refine)
+    auto run_batch = [&](const unsigned* begin) -> int {
+        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, begin + 0, ctx->d_ctr + 0,
+                                   ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, sB));
+        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, begin + 1, ctx->d_ctr + 1,
+                                   ctx->cap_raw, ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2,
+                                   ctx->cap_ori, sB));
+        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, begin + 2, ctx->d_ctr + 2,
+                                       ctx->cap_ori, out_desc_f32 ? ctx->d_df32 : nullptr, sB));
+        return SIFT_OK;
+    };
+    const unsigned* batch0 = ctx->d_ctr + 4;
+    unsigned* batch1 = ctx->d_ctr + 8;
     for (int o = 0; o < o_small; ++o) {
         for (int l = 1; l < g.n_gauss; ++l) {
             const bool dec = (l == dec_level) && (o + 1 < g.octaves);
@@ -247,64 +316,76 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
                              dec ? g.W[o + 1] : 0, dec ? g.H[o + 1] : 0);
             if (st != SIFT_OK) return st;
         }
+        hipEvent_t done = sync_event(ctx, ev_i++);
+        if (!done) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(hipEventRecord(done, sA));
+        SIFT_HIP_TRY(hipStreamWaitEvent(sB, done, 0));
+        if (tiles) {
+            const ExtremaGrid eg = extrema_grid(g, o, o + 1);
+            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
+                                              ctx->d_ctr + 0, ctx->cap_cand, sB));
+        } else {
+            SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
+                                            p->window_size, dp.threshold, ctx->d_cand,
+                                            ctx->d_ctr + 0, ctx->cap_cand, sB));
+        }
     }
     if (o_small < g.octaves) {
-        hipEvent_t ea = nullptr, eb = nullptr;
-        if (ctx->profiling) {
-            ea = next_event(ctx);
-            eb = next_event(ctx);
-            if (!ea || !eb) return SIFT_ERR_HIP;
-            SIFT_HIP_TRY(hipEventRecord(ea, ctx->stream));
+        double bytes = 0.0;
+        for (int o = o_small; o < g.octaves; ++o) {
+            bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[o] * (double)g.H[o];
+            if (o + 1 < g.octaves) bytes += 8.0 * (double)g.W[o + 1] * (double)g.H[o + 1];
         }
+        hipEvent_t e0, e1;
+        if (prof_events(ctx, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(ctx->d_pt, o_small, g.octaves - 1, g.n_gauss,
-                                        ctx->d_taps, ctx->stream));
-        if (ctx->profiling) {
-            SIFT_HIP_TRY(hipEventRecord(eb, ctx->stream));
-            double bytes = 0.0;
-            for (int o = o_small; o < g.octaves; ++o) {
-                bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[o] * (double)g.H[o];
-                if (o + 1 < g.octaves) bytes += 8.0 * (double)g.W[o + 1] * (double)g.H[o + 1];
-            }
-            ctx->pending.push_back({ea, eb, bytes});
-        }
+                                        ctx->d_taps, sA, e0, e1));
     }
-
-    // extrema tile grid (window_size 3): every octave in one launch
-    ExtremaGrid eg;
-    std::memset(&eg, 0, sizeof eg);
-    eg.octaves = g.octaves;
-    for (int o = 0; o < g.octaves; ++o) {
-        const int tx = g.W[o] > 2 ? (g.W[o] - 2 + 63) / 64 : 0;
-        const int ty = g.H[o] > 2 ? (g.H[o] - 2 + 15) / 16 : 0;
-        eg.tiles_x[o] = tx > 0 ? tx : 1;
-        eg.first_tile[o + 1] = eg.first_tile[o] + tx * ty;
-    }
-
-    // ---- extrema -> refine -> orientation -> descriptor, re-run on overflow
-    clk::time_point t_enq, t_wait;
-    for (int attempt = 0;; ++attempt) {
-        SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, 4 * sizeof(unsigned), ctx->stream));
-        if (p->window_size / 2 == 1) {
-            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold,
-                                              ctx->d_cand, ctx->d_ctr + 0, ctx->cap_cand,
-                                              ctx->stream));
+    // batch 0: keypoints of the large octaves, while stream A still runs the
+    // single-workgroup small-octave kernel
+    if (o_small > 0 && (st = run_batch(batch0)) != SIFT_OK) return st;
+    if (o_small < g.octaves) {
+        // batch 1: the small octaves, from a snapshot of the counters
+        SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, batch1, sB));
+        hipEvent_t done = sync_event(ctx, ev_i++);
+        if (!done) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(hipEventRecord(done, sA));
+        SIFT_HIP_TRY(hipStreamWaitEvent(sB, done, 0));
+        if (tiles) {
+            const ExtremaGrid eg = extrema_grid(g, o_small, g.octaves);
+            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
+                                              ctx->d_ctr + 0, ctx->cap_cand, sB));
         } else {
-            for (int o = 0; o < g.octaves; ++o)
+            for (int o = o_small; o < g.octaves; ++o)
                 SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
                                                 p->window_size, dp.threshold, ctx->d_cand,
-                                                ctx->d_ctr + 0, ctx->cap_cand, ctx->stream));
+                                                ctx->d_ctr + 0, ctx->cap_cand, sB));
         }
-        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, ctx->d_ctr + 0, ctx->cap_cand,
-                                   ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, ctx->stream));
-        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw,
-                                   ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2, ctx->cap_ori,
-                                   ctx->stream));
-        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, ctx->d_ctr + 2, ctx->cap_ori,
-                                       out_desc_f32 ? ctx->d_df32 : nullptr, ctx->stream));
+        if ((st = run_batch(batch1)) != SIFT_OK) return st;
+    }
+
+    // ---- wait for the counters; re-run every candidate stage on overflow
+    clk::time_point t_enq, t_wait;
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 0) {  // pyramid is complete; one batch over everything
+            SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sB));
+            if (tiles) {
+                const ExtremaGrid eg = extrema_grid(g, 0, g.octaves);
+                SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold,
+                                                  ctx->d_cand, ctx->d_ctr + 0, ctx->cap_cand,
+                                                  sB));
+            } else {
+                for (int o = 0; o < g.octaves; ++o)
+                    SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
+                                                    p->window_size, dp.threshold, ctx->d_cand,
+                                                    ctx->d_ctr + 0, ctx->cap_cand, sB));
+            }
+            if ((st = run_batch(batch0)) != SIFT_OK) return st;
+        }
         SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
-                                    hipMemcpyDeviceToHost, ctx->stream));
+                                    hipMemcpyDeviceToHost, sB));
         t_enq = clk::now();
-        SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+        SIFT_HIP_TRY(hipStreamSynchronize(sB));
         t_wait = clk::now();
         const unsigned nc = ctx->h_ctr[0], nr = ctx->h_ctr[1], no = ctx->h_ctr[2];
         if (nc <= ctx->cap_cand && nr <= ctx->cap_raw && no <= ctx->cap_ori) break;
@@ -328,18 +409,18 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     if ((st = ctx->h_off0.ensure(n_ori)) != SIFT_OK) return st;
     if (n_ori) {
         SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.p, ctx->d_ori, n_ori * sizeof(sift_kp),
-                                    hipMemcpyDeviceToHost, ctx->stream));
+                                    hipMemcpyDeviceToHost, ctx->stream2));
         SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.p, ctx->d_off0, n_ori * sizeof(double),
-                                    hipMemcpyDeviceToHost, ctx->stream));
+                                    hipMemcpyDeviceToHost, ctx->stream2));
     }
     if (out_desc_f32) {
         if ((st = ctx->h_df32.ensure((size_t)n_ori * 128)) != SIFT_OK) return st;
         if (n_ori)
             SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.p, ctx->d_df32,
                                         (size_t)n_ori * 128 * sizeof(float),
-                                        hipMemcpyDeviceToHost, ctx->stream));
+                                        hipMemcpyDeviceToHost, ctx->stream2));
     }
-    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream2));
     const auto t_copy = clk::now();
 
     if (ctx->profiling) {
@@ -355,7 +436,8 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
 
     // final size with glibc pow + clean_keypoints, in the g++-built layer
     ctx->keep.resize(n_ori);
-    const size_t n = host_finalize(p, ctx->h_ori.p, ctx->h_off0.p, n_ori, ctx->keep.data());
+    const size_t n = host_finalize(p, ctx->h_ori.p, ctx->h_off0.p, n_ori, ctx->keep.data(),
+                                   &ctx->fin_ws);
     const auto t_fin = clk::now();
 
     sift_kp* kps = (sift_kp*)std::malloc(std::max<size_t>(n, 1) * sizeof(sift_kp));
@@ -427,7 +509,8 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (!ctx) return SIFT_ERR_NOMEM;
     ctx->device = device;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&ctx->d_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&ctx->d_ctr, kCtrWords * sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&ctx->h_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&ctx->h_stage, sizeof(Stage)) != hipSuccess ||
         hipMalloc(&ctx->d_stage, sizeof(Stage)) != hipSuccess ||
@@ -445,6 +528,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
     if (!ctx) return SIFT_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     void* bufs[] = {ctx->d_in, ctx->d_pyr, ctx->d_tmp, ctx->d_cand, ctx->d_raw,
                     ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_stage};
     for (void* b : bufs)
@@ -455,7 +539,9 @@ int sift_hip_destroy(sift_ctx* ctx) {
     ctx->h_off0.release();
     ctx->h_df32.release();
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     delete ctx;
     return SIFT_OK;
 }

@@ -107,36 +107,63 @@ int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* 
 }
 
 size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
-                     unsigned* keep) {
+                     unsigned* keep, FinalizeWorkspace* ws) {
     for (unsigned i = 0; i < n; ++i) {
         sift_kp& r = recs[i];
-        const double scale = std::pow(2, r.octave);
+        // std::pow(2, octave) is exactly 2^octave; ldexp gives the same value
+        const double scale = std::ldexp(1.0, r.octave);
         double size = p->init_sigma * scale *
                       std::pow(2, (static_cast<double>(r.layer) + off0[i]) / p->intervals);
         if (p->double_image_size) size /= 2;
         r.size = size;
     }
-    // sort a compact key array (40 B per record) rather than indices into
-    // the 168-byte records: same comparator, cache-friendly
-    struct Key {
-        double x, y, size, pori;
-        int octave;
-        unsigned idx;
-    };
-    std::vector<Key> keys(n);
-    for (unsigned i = 0; i < n; ++i)
-        keys[i] = {recs[i].x, recs[i].y, recs[i].size, recs[i].pori, recs[i].octave, i};
-    // Keypoint::operator< (sift.hh:31-41)
-    std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) {
+    // Sort a compact key array (40 B per record) in Keypoint::operator<
+    // order (sift.hh:31-41: x asc, y asc, size desc, pori asc, octave desc).
+    // x >= 0 for every keypoint, and b(x) = x / x_max * B is monotone
+    // non-decreasing under round-to-nearest, so a stable bucket pass on b(x)
+    // followed by a comparator sort inside each (tiny) bucket yields exactly
+    // the order std::sort with the full comparator would, in O(n + B).
+    using Key = FinalizeKey;
+    auto less = [](const Key& a, const Key& b) {
         if (a.x != b.x) return a.x < b.x;
         if (a.y != b.y) return a.y < b.y;
         if (a.size != b.size) return a.size > b.size;
         if (a.pori != b.pori) return a.pori < b.pori;
         return a.octave > b.octave;
-    });
+    };
+    // workspace reused across calls (no per-call allocation / page faults)
+    std::vector<Key>& keys = ws->keys;
+    std::vector<Key>& sorted = ws->sorted;
+    keys.resize(n);
+    sorted.resize(n);
+    double x_max = 0.0;
+    for (unsigned i = 0; i < n; ++i) {
+        keys[i] = {recs[i].x, recs[i].y, recs[i].size, recs[i].pori, recs[i].octave, i};
+        x_max = std::max(x_max, recs[i].x);
+    }
+    const size_t B = std::max<size_t>(1, std::min<size_t>(n, (size_t)1 << 20));
+    std::vector<unsigned>& start = ws->start;
+    start.assign(B + 1, 0);
+    auto bucket = [&](double x) -> size_t {
+        if (!(x_max > 0.0)) return 0;
+        const double f = x / x_max * (double)B;
+        return f >= (double)(B - 1) ? B - 1 : (f <= 0.0 ? 0 : (size_t)f);
+    };
+    for (unsigned i = 0; i < n; ++i) ++start[bucket(keys[i].x) + 1];
+    for (size_t b = 0; b < B; ++b) start[b + 1] += start[b];
+    {
+        std::vector<unsigned>& fill = ws->fill;
+        fill.assign(start.begin(), start.end() - 1);
+        for (unsigned i = 0; i < n; ++i) sorted[fill[bucket(keys[i].x)]++] = keys[i];
+    }
+    for (size_t b = 0; b < B; ++b) {
+        Key* lo = sorted.data() + start[b];
+        Key* hi = sorted.data() + start[b + 1];
+        if (hi - lo > 1) std::sort(lo, hi, less);
+    }
     size_t m = 0;
     for (unsigned i = 0; i < n; ++i) {
-        const Key& k = keys[i];
+        const Key& k = sorted[i];
         if (m > 0) {
             // std::unique compares with the last kept element (Keypoint::
             // operator==, sift.hh:25-27: x, y, size, pori)

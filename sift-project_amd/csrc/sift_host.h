@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstddef>
+#include <vector>
 
 #include "sift_types.h"
 
@@ -32,7 +33,16 @@ int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* 
 // sift.cpp:525) written into recs[i].size, then clean_keypoints
 // (sift.cpp:20-24): indices of the sorted, de-duplicated records go to keep[]
 // (capacity n). Returns the number kept.
+struct FinalizeKey {
+    double x, y, size, pori;
+    int octave;
+    unsigned idx;
+};
+struct FinalizeWorkspace {  // reused across calls
+    std::vector<FinalizeKey> keys, sorted;
+    std::vector<unsigned> start, fill;
+};
 size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
-                     unsigned* keep);
+                     unsigned* keep, FinalizeWorkspace* ws);
 
 }  // namespace sift_amd

@@ -15,25 +15,36 @@ hipError_t prepare_kernel_attributes();
 
 hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double* out,
                           int W0, int H0, hipStream_t s);
+// e0/e1: optional HIP events timestamped by the dispatch itself (profiling)
 hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurTaps& taps,
-                       double* dec, int Wd, int Hd, double* tmp, hipStream_t s);
+                       double* dec, int Wd, int Hd, double* tmp, hipStream_t s, hipEvent_t e0,
+                       hipEvent_t e1);
+// Initial blur fused with gray/bilinear-x2 staging from the input image.
+// Returns false (nothing launched) when the fused path does not apply.
+bool launch_blur_initial_fused(const double* in, int w, int h, int c, int dbl, double* dst,
+                               int W0, int H0, const BlurTaps& taps, hipStream_t s,
+                               hipEvent_t e0, hipEvent_t e1, hipError_t* err);
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
-                              const BlurTaps* d_taps, hipStream_t s);
+                              const BlurTaps* d_taps, hipStream_t s, hipEvent_t e0,
+                              hipEvent_t e1);
 hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
                                 int thr, sift_extremum* out, unsigned* counter, unsigned cap,
                                 hipStream_t s);
 hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
                               int window_size, int thr, sift_extremum* out, unsigned* counter,
                               unsigned cap, hipStream_t s);
-hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P,
-                         const sift_extremum* cand, const unsigned* n_cand, unsigned cap_cand,
+// Keypoint stages process the index range [*begin, *end) of their input
+// list (device counters), so a detect can run them in batches.
+hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s);
+hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
+                         const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s);
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
-                         const unsigned* n_raw, unsigned cap_raw, sift_kp* out,
-                         double* out_off0, unsigned* n_out, unsigned cap_out,
+                         const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
+                         sift_kp* out, double* out_off0, unsigned* n_out, unsigned cap_out,
                          hipStream_t s);
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
-                             const unsigned* n, unsigned cap, float* desc_f32,
-                             hipStream_t s);
+                             const unsigned* rec_begin, const unsigned* n, unsigned cap,
+                             float* desc_f32, hipStream_t s);
 
 }  // namespace sift_amd

@@ -12,6 +12,7 @@
 // (image_io.cpp:81-92). DoG planes are never materialised: D_l = G_{l+1} -
 // G_l is one IEEE subtraction, recomputed bit-identically where needed
 // (sift.cpp:209-225, image.cpp:30-36).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -39,6 +40,46 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) {
 
 // 2^e for small integer e, exact (the reference uses std::pow(2, int)).
 __device__ __forceinline__ double pow2i(int e) { return ldexp(1.0, e); }
+
+// XCD-aware block remap (bijective): workgroups are dealt round-robin over
+// the 8 XCDs, so consecutive block ids land on different L2s. Renumber so
+// every XCD owns one contiguous range of logical tiles; neighbouring strips
+// (which re-read each other's halo columns / priming rows) then share an L2.
+// Placement is a speed hint only; results do not depend on it.
+__device__ __forceinline__ void xcd_remap(int& bx, int& by) {
+    const int nx = gridDim.x;
+    const int n = gridDim.x * gridDim.y;
+    const int orig = blockIdx.y * nx + blockIdx.x;
+    const int q = n / 8, r = n % 8, xcd = orig % 8;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+    bx = id % nx;
+    by = id / nx;
+}
+
+// Source of the rows staged by k_blur: a Gaussian plane, or — for the
+// initial blur — the reference's initial image computed on the fly from the
+// input: convert_to_grayscale (image.cpp:8-24) and, with double_image_size,
+// resize_inter_bilinear x2 (image.cpp:62-88); bit-identical to materialising
+// it first (same expressions, evaluated once per staged pixel).
+enum BlurSrcMode { kSrcPlane = 0, kSrcGray = 1, kSrcUpsample = 2 };
+
+template <int MODE>
+__device__ __forceinline__ double fetch_src(const BlurSource& s, int W, int yy, int gx) {
+    if (MODE == kSrcPlane) return s.p[(size_t)yy * W + gx];
+    auto gray = [&](int x, int y) -> double {
+        const double* q = s.p + ((size_t)y * s.w + x) * s.c;
+        if (s.c == 1) return q[0];
+        return 0.2126 * q[0] + 0.7152 * q[1] + 0.0722 * q[2];
+    };
+    if (MODE == kSrcGray) return gray(gx, yy);
+    const double fx = gx / 2.0, fy = yy / 2.0;
+    const int x0 = (int)fx, y0 = (int)fy;
+    const int x1 = min(x0 + 1, s.w - 1), y1 = min(y0 + 1, s.h - 1);
+    const double dx = fx - x0, dy = fy - y0;
+    const double v0 = gray(x0, y0) * (1 - dx) + gray(x1, y0) * dx;
+    const double v1 = gray(x0, y1) * (1 - dx) + gray(x1, y1) * dx;
+    return v0 * (1 - dy) + v1 * dy;
+}
 
 }  // namespace
 
@@ -87,18 +128,19 @@ __global__ __launch_bounds__(256) void k_prepare(const double* __restrict__ in, 
 // 200-203). DECIM additionally writes resize_inter_nearest (image.cpp:41-55)
 // of the output, i.e. the next octave's base (sift.cpp:195-196).
 // ---------------------------------------------------------------------------
-template <int R, bool DECIM>
-__global__ __launch_bounds__(256) void k_blur(const double* __restrict__ src,
-                                              double* __restrict__ dst, int W, int H,
-                                              int rows, BlurTaps taps,
+template <int R, bool DECIM, int MODE>
+__global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict__ dst, int W,
+                                              int H, int rows, BlurTaps taps,
                                               double* __restrict__ dec, int Wd, int Hd) {
     constexpr int NW = 2 * R + 1;  // register window depth
     constexpr int SEG = 64 + 2 * R;
     __shared__ double sline[4][SEG];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int x0 = blockIdx.x * 64;
-    const int y_begin = (blockIdx.y * 4 + wv) * rows;
+    int bx, by;
+    xcd_remap(bx, by);
+    const int x0 = bx * 64;
+    const int y_begin = (by * 4 + wv) * rows;
     if (y_begin >= H) return;  // whole wave leaves; no block barriers below
     const int y_end = min(y_begin + rows, H);
     double* sl = sline[wv];
@@ -117,9 +159,8 @@ __global__ __launch_bounds__(256) void k_blur(const double* __restrict__ src,
     for (int q = 0; q < NW; ++q) win[q] = 0.0;
 
     const int yy0 = y_begin - R, yy_end = y_end + R;
-    const double* srow = src + (size_t)clampi(yy0, 0, H - 1) * W;
-    double a0 = srow[gx0];
-    double a1 = has1 ? srow[gx1] : 0.0;
+    double a0 = fetch_src<MODE>(src, W, clampi(yy0, 0, H - 1), gx0);
+    double a1 = has1 ? fetch_src<MODE>(src, W, clampi(yy0, 0, H - 1), gx1) : 0.0;
     // The row loop is unrolled by NW so that the window slot of every row is
     // a compile-time constant: slot s of block yb holds horizontal-pass row
     // yb+s, and no register moves are needed to slide the window.
@@ -131,9 +172,9 @@ __global__ __launch_bounds__(256) void k_blur(const double* __restrict__ src,
                 sl[lane] = a0;
                 if (has1) sl[64 + lane] = a1;
                 if (yy + 1 < yy_end) {  // prefetch the next source row
-                    const double* nrow = src + (size_t)clampi(yy + 1, 0, H - 1) * W;
-                    a0 = nrow[gx0];
-                    if (has1) a1 = nrow[gx1];
+                    const int ny = clampi(yy + 1, 0, H - 1);
+                    a0 = fetch_src<MODE>(src, W, ny, gx0);
+                    if (has1) a1 = fetch_src<MODE>(src, W, ny, gx1);
                 }
                 wave_sync();
                 // horizontal pass (image.cpp:170-185)
@@ -168,62 +209,132 @@ __global__ __launch_bounds__(256) void k_blur(const double* __restrict__ src,
 // live in LDS, so each level is two barrier-separated LDS sweeps instead of
 // a latency-bound launch; each finished level is streamed to its global
 // plane (needed later by extrema/orientation/descriptor), and the decimated
-// level `intervals` becomes the next octave's base in LDS. Same arithmetic
-// and order as k_blur (image.cpp:156-214), replicate borders by clamping.
+// level `intervals` becomes the next octave's base in LDS (all three regions:
+// kLdsOctaveBytes). Same arithmetic and order as k_blur (image.cpp:156-214),
+// replicate borders by clamping. 16 waves sweep 16 rows x 64 columns at a
+// time; the radius is a template parameter so the taps sit in registers.
 // ---------------------------------------------------------------------------
+struct LdsLevel {
+    double* A;  // current level (in: previous level, out: this level)
+    double* T;  // horizontal-pass temporary
+    double* D;  // next octave base (when dec)
+    double* g;  // global plane of this level
+    double* gd; // global plane of the next octave's base (when dec)
+    int W, H, Wd, Hd;
+    bool dec;
+};
+
+template <int R>
+__device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    double k[R + 1];
+#pragma unroll
+    for (int u = 0; u <= R; ++u) k[u] = t.k[u];
+    const double sw = t.sum_w;
+    const int W = L.W, H = L.H;
+    for (int y = ty; y < H; y += 16) {
+        const double* row = L.A + y * W;
+        for (int x = tx; x < W; x += 64) {
+            double acc = row[x] * k[0];
+#pragma unroll
+            for (int u = 1; u <= R; ++u) acc += k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
+            L.T[y * W + x] = acc / sw;
+        }
+    }
+    __syncthreads();
+    for (int y = ty; y < H; y += 16) {
+        for (int x = tx; x < W; x += 64) {
+            double acc = L.T[y * W + x] * k[0];
+#pragma unroll
+            for (int u = 1; u <= R; ++u)
+                acc += k[u] * (L.T[min(y + u, H - 1) * W + x] + L.T[max(y - u, 0) * W + x]);
+            const double v = acc / sw;
+            L.A[y * W + x] = v;
+            L.g[y * W + x] = v;
+            if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
+                L.D[(y >> 1) * L.Wd + (x >> 1)] = v;
+                L.gd[(y >> 1) * L.Wd + (x >> 1)] = v;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int W = L.W, H = L.H, R = t.R;
+    for (int y = ty; y < H; y += 16) {
+        const double* row = L.A + y * W;
+        for (int x = tx; x < W; x += 64) {
+            double acc = row[x] * t.k[0];
+            for (int u = 1; u <= R; ++u) acc += t.k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
+            L.T[y * W + x] = acc / t.sum_w;
+        }
+    }
+    __syncthreads();
+    for (int y = ty; y < H; y += 16) {
+        for (int x = tx; x < W; x += 64) {
+            double acc = L.T[y * W + x] * t.k[0];
+            for (int u = 1; u <= R; ++u)
+                acc += t.k[u] * (L.T[min(y + u, H - 1) * W + x] + L.T[max(y - u, 0) * W + x]);
+            const double v = acc / t.sum_w;
+            L.A[y * W + x] = v;
+            L.g[y * W + x] = v;
+            if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
+                L.D[(y >> 1) * L.Wd + (x >> 1)] = v;
+                L.gd[(y >> 1) * L.Wd + (x >> 1)] = v;
+            }
+        }
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
                                                       int o_first, int o_last, int n_gauss,
                                                       const BlurTaps* __restrict__ taps) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, nt = blockDim.x;
     const int dec_level = n_gauss - 3;
-    int W = pt->w[o_first], H = pt->h[o_first];
     double* A = lds;                         // current level
     double* T = lds + kLdsOctavePx;          // horizontal-pass temporary
     double* D = lds + 2 * kLdsOctavePx;      // next octave's base
     {
+        const int W = pt->w[o_first], H = pt->h[o_first];
         const double* g0 = pt->lvl[o_first][0];
         for (int i = tid; i < W * H; i += nt) A[i] = g0[i];
     }
     __syncthreads();
     for (int o = o_first; o <= o_last; ++o) {
-        W = pt->w[o];
-        H = pt->h[o];
-        const int N = W * H;
         const bool has_next = o < o_last;
-        const int Wd = has_next ? pt->w[o + 1] : 0, Hd = has_next ? pt->h[o + 1] : 0;
+        LdsLevel L;
+        L.A = A;
+        L.T = T;
+        L.D = D;
+        L.W = pt->w[o];
+        L.H = pt->h[o];
+        L.Wd = has_next ? pt->w[o + 1] : 0;
+        L.Hd = has_next ? pt->h[o + 1] : 0;
+        L.gd = has_next ? pt->lvl[o + 1][0] : nullptr;
         for (int l = 1; l < n_gauss; ++l) {
+            L.g = pt->lvl[o][l];
+            L.dec = has_next && l == dec_level;
             const BlurTaps& t = taps[l];
-            const int R = t.R;
-            const double sw = t.sum_w;
-            for (int i = tid; i < N; i += nt) {
-                const int y = i / W, x = i - y * W;
-                const double* row = A + y * W;
-                double acc = row[x] * t.k[0];
-                for (int u = 1; u <= R; ++u)
-                    acc += t.k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
-                T[i] = acc / sw;
+            switch (t.R) {
+#define SIFT_LDS_CASE(RR) \
+    case RR:              \
+        lds_level<RR>(L, t); \
+        break;
+                SIFT_LDS_CASE(1) SIFT_LDS_CASE(2) SIFT_LDS_CASE(3) SIFT_LDS_CASE(4)
+                SIFT_LDS_CASE(5) SIFT_LDS_CASE(6) SIFT_LDS_CASE(7) SIFT_LDS_CASE(8)
+                SIFT_LDS_CASE(9) SIFT_LDS_CASE(10) SIFT_LDS_CASE(11) SIFT_LDS_CASE(12)
+                SIFT_LDS_CASE(13) SIFT_LDS_CASE(14) SIFT_LDS_CASE(15) SIFT_LDS_CASE(16)
+#undef SIFT_LDS_CASE
+                default:
+                    lds_level_any(L, t);
             }
-            __syncthreads();
-            double* g = pt->lvl[o][l];
-            for (int i = tid; i < N; i += nt) {
-                const int y = i / W, x = i - y * W;
-                double acc = T[i] * t.k[0];
-                for (int u = 1; u <= R; ++u)
-                    acc += t.k[u] * (T[min(y + u, H - 1) * W + x] + T[max(y - u, 0) * W + x]);
-                const double v = acc / sw;
-                A[i] = v;
-                g[i] = v;
-                if (has_next && l == dec_level && !(x & 1) && !(y & 1) && (x >> 1) < Wd &&
-                    (y >> 1) < Hd) {
-                    D[(y >> 1) * Wd + (x >> 1)] = v;
-                    pt->lvl[o + 1][0][(y >> 1) * Wd + (x >> 1)] = v;
-                }
-            }
-            __syncthreads();
         }
         if (has_next) {
-            for (int i = tid; i < Wd * Hd; i += nt) A[i] = D[i];
+            for (int i = tid; i < L.Wd * L.Hd; i += nt) A[i] = D[i];
             __syncthreads();
         }
     }
@@ -267,14 +378,14 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
 // or v == min(cube): v is itself in the cube, so the centre comparison is
 // vacuous (sift.cpp:241-246). DoG values are G_{l+1} - G_l computed on the fly.
 // ---------------------------------------------------------------------------
-// Tiled variant used for window_size 3: ONE launch covers every octave.
-// A 256-thread workgroup owns a 64x16 block of centre pixels of one octave;
-// it stages the (66x18)-pixel DoG halo tile of every DoG layer in LDS (six
-// Gaussian loads per staged pixel, all independent, so a tile costs one
-// memory round trip), then each thread takes one column x four centre rows:
-// per layer it forms 3-wide row max/min over six staged rows and the 3x3
-// max/min of its four centres in registers. Candidates are compacted with a
-// 64-bit ballot per (row, layer) and one atomic per wave.
+// Tiled variant used for window_size 3 (one launch per octave set).
+// A 256-thread workgroup owns a 64x16 block of centre pixels of one octave:
+// it stages the (66x18)-pixel DoG halo tile of every DoG layer in LDS (all
+// Gaussian loads of a thread issued before any is used, so a tile costs one
+// memory round trip), then each thread takes one column x four centre rows
+// and walks the layers with a rolling window of three layers' 3x3 max/min
+// in registers. Candidates are compacted with a 64-bit ballot per
+// (row, layer) and one atomic per wave.
 template <int NL>
 __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restrict__ pt,
                                                        ExtremaGrid eg, int thr,
@@ -283,34 +394,47 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
                                                        unsigned cap) {
     constexpr int ND = NL - 1;
     constexpr int TW = 64, TH = 16, SW = TW + 2, SH = TH + 2;
+    constexpr int NPIX = SW * SH;             // 1188 staged pixels
+    constexpr int NIT = (NPIX + 255) / 256;   // 5 per thread
     __shared__ double sd[ND][SH][SW];
     const int tid = threadIdx.x, lane = tid & 63;
-    int o = 0;
-    while (o + 1 < eg.octaves && (int)blockIdx.x >= eg.first_tile[o + 1]) ++o;
-    const int tile = blockIdx.x - eg.first_tile[o];
-    const int tx = tile % eg.tiles_x[o], ty = tile / eg.tiles_x[o];
+    int e = 0;
+    while (e + 1 < eg.n && (int)blockIdx.x >= eg.first_tile[e + 1]) ++e;
+    const int o = eg.oct[e];
+    const int tile = blockIdx.x - eg.first_tile[e];
+    const int tx = tile % eg.tiles_x[e], ty = tile / eg.tiles_x[e];
     const int W = pt->w[o], H = pt->h[o];
     const int cx0 = 1 + tx * TW, cy0 = 1 + ty * TH;  // first centre of the tile
-    const double* G[NL];
+    {
+        double g[NIT][NL];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) G[l] = pt->lvl[o][l];
-    for (int i = tid; i < SH * SW; i += 256) {
-        const int r = i / SW, c = i - r * SW;
-        const size_t q = (size_t)clampi(cy0 - 1 + r, 0, H - 1) * W + clampi(cx0 - 1 + c, 0, W - 1);
-        double g[NL];
+        for (int it = 0; it < NIT; ++it) {
+            const int i = tid + it * 256;
+            const int r = i / SW, c = i - r * SW;
+            const size_t q = (size_t)clampi(cy0 - 1 + r, 0, H - 1) * W + clampi(cx0 - 1 + c, 0, W - 1);
 #pragma unroll
-        for (int l = 0; l < NL; ++l) g[l] = G[l][q];
+            for (int l = 0; l < NL; ++l) g[it][l] = (i < NPIX) ? pt->lvl[o][l][q] : 0.0;
+        }
 #pragma unroll
-        for (int l = 0; l < ND; ++l) sd[l][r][c] = g[l + 1] - g[l];
+        for (int it = 0; it < NIT; ++it) {
+            const int i = tid + it * 256;
+            if (i < NPIX) {
+                const int r = i / SW, c = i - r * SW;
+#pragma unroll
+                for (int l = 0; l < ND; ++l) sd[l][r][c] = g[it][l + 1] - g[it][l];
+            }
+        }
     }
     __syncthreads();
     const int c = lane;              // centre column in the tile
     const int r0 = (tid >> 6) * 4;   // first of this thread's four centre rows
     const int x = cx0 + c;
-    double cmax[ND][4], cmin[ND][4];
+    const double dthr = (double)thr;
+    // rolling 3x3 max/min of layers l-2 (p), l-1 (q), l (n) for 4 centres
+    double pmx[4], pmn[4], qmx[4], qmn[4];
 #pragma unroll
     for (int l = 0; l < ND; ++l) {
-        double rmx[6], rmn[6];
+        double rmx[6], rmn[6], nmx[4], nmn[4];
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
             const double a = sd[l][r0 + r][c], b = sd[l][r0 + r][c + 1], d = sd[l][r0 + r][c + 2];
@@ -319,32 +443,37 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            cmax[l][k] = fmax(fmax(rmx[k], rmx[k + 1]), rmx[k + 2]);
-            cmin[l][k] = fmin(fmin(rmn[k], rmn[k + 1]), rmn[k + 2]);
+            nmx[k] = fmax(fmax(rmx[k], rmx[k + 1]), rmx[k + 2]);
+            nmn[k] = fmin(fmin(rmn[k], rmn[k + 1]), rmn[k + 2]);
         }
-    }
-    const double dthr = (double)thr;
+        if (l >= 2) {
+            const int z = l - 1;  // centre layer of the p, q, n window
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int y = cy0 + r0 + k;
-        const bool in = x < W - 1 && y < H - 1;
+            for (int k = 0; k < 4; ++k) {
+                const int y = cy0 + r0 + k;
+                const double v = sd[z][r0 + k + 1][c + 1];
+                bool cand = false;
+                if (x < W - 1 && y < H - 1 && fabs(v) > dthr) {
+                    const double mx = fmax(fmax(pmx[k], qmx[k]), nmx[k]);
+                    const double mn = fmin(fmin(pmn[k], qmn[k]), nmn[k]);
+                    cand = (v == mx) || (v == mn);
+                }
+                const unsigned long long m = __ballot(cand);
+                if (m) {
+                    unsigned base = 0;
+                    if (lane == 0) base = atomicAdd(counter, (unsigned)__popcll(m));
+                    base = __shfl(base, 0);
+                    const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                    if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, o};
+                }
+            }
+        }
 #pragma unroll
-        for (int z = 1; z < ND - 1; ++z) {
-            const double v = sd[z][r0 + k + 1][c + 1];
-            bool cand = false;
-            if (in && fabs(v) > dthr) {
-                const double mx = fmax(fmax(cmax[z - 1][k], cmax[z][k]), cmax[z + 1][k]);
-                const double mn = fmin(fmin(cmin[z - 1][k], cmin[z][k]), cmin[z + 1][k]);
-                cand = (v == mx) || (v == mn);
-            }
-            const unsigned long long m = __ballot(cand);
-            if (m) {
-                unsigned base = 0;
-                if (lane == 0) base = atomicAdd(counter, (unsigned)__popcll(m));
-                base = __shfl(base, 0);
-                const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-                if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, o};
-            }
+        for (int k = 0; k < 4; ++k) {
+            pmx[k] = qmx[k];
+            pmn[k] = qmn[k];
+            qmx[k] = nmx[k];
+            qmn[k] = nmn[k];
         }
     }
 }
@@ -386,13 +515,15 @@ __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict_
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt, DevParams P,
                                                 const sift_extremum* __restrict__ cand,
+                                                const unsigned* __restrict__ cand_begin,
                                                 const unsigned* __restrict__ n_cand,
                                                 unsigned cap_cand, RawKp* __restrict__ out,
                                                 unsigned* __restrict__ n_out,
                                                 unsigned cap_out) {
     const unsigned n = min(*n_cand, cap_cand);
+    const unsigned i0 = min(*cand_begin, n);
     const int b = P.window_size / 2;
-    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+    for (unsigned i = i0 + blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += gridDim.x * blockDim.x) {
         const sift_extremum e = cand[i];
         const int o = e.octave;
@@ -489,8 +620,10 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
 //  * The in-place circular smoothing (sift.cpp:496-504) is a Gauss-Seidel
 //    recurrence and runs on lane 0 with the running value in a register.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt, DevParams P,
+template <bool WIDE>  // WIDE: more than 64 orientation bins (up to kMaxBins)
+__global__ __launch_bounds__(256, 3) void k_orient(const PyrTable* __restrict__ pt, DevParams P,
                                                 const RawKp* __restrict__ raw,
+                                                const unsigned* __restrict__ raw_begin,
                                                 const unsigned* __restrict__ n_raw,
                                                 unsigned cap_raw, sift_kp* __restrict__ out,
                                                 double* __restrict__ out_off0,
@@ -503,9 +636,10 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const unsigned n = min(*n_raw, cap_raw);
+    const unsigned k0 = min(*raw_begin, n);
     const int nb = P.num_bins;
-    const int nbq = (nb + 63) >> 6;
-    for (unsigned k = blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
+    const int nbq = WIDE ? (nb + 63) >> 6 : 1;
+    for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
         const RawKp kp = raw[k];
         const int o = kp.octave;
         const double inv = 1.0 / pow2i(o);
@@ -566,7 +700,7 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
                 for (int e = 0; e < 8; ++e) {
                     // adding +0.0 never changes a non-negative bin sum
                     hb[0] += (bs[e] == lane) ? vs[e] : 0.0;
-                    if (nbq > 1) {
+                    if (WIDE && nbq > 1) {
                         hb[1] += (bs[e] == lane + 64) ? vs[e] : 0.0;
                         if (nbq > 2) {
                             hb[2] += (bs[e] == lane + 128) ? vs[e] : 0.0;
@@ -665,6 +799,7 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__ pt,
                                                     DevParams P, sift_kp* __restrict__ recs,
+                                                    const unsigned* __restrict__ rec_begin,
                                                     const unsigned* __restrict__ n_p,
                                                     unsigned cap,
                                                     float* __restrict__ desc_f32) {
@@ -676,7 +811,8 @@ __global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const unsigned n = min(*n_p, cap);
-    for (unsigned k = blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
+    const unsigned k0 = min(*rec_begin, n);
+    for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
         const double* hdr = reinterpret_cast<const double*>(&recs[k]);
         const double kx = hdr[0], ky = hdr[1];
         const int o = reinterpret_cast<const int*>(hdr)[4];
@@ -824,32 +960,46 @@ __global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__
 // ---------------------------------------------------------------------------
 // launch helpers
 // ---------------------------------------------------------------------------
-template <int R>
-static hipError_t launch_blur_r(const double* src, double* dst, int W, int H, int rows,
-                                const BlurTaps& taps, double* dec, int Wd, int Hd,
-                                hipStream_t s) {
-    dim3 grid((W + 63) / 64, ((H + rows - 1) / rows + 3) / 4);
-    if (dec)
-        hipLaunchKernelGGL((k_blur<R, true>), grid, dim3(256), 0, s, src, dst, W, H, rows,
-                           taps, dec, Wd, Hd);
+template <class K, class... Args>
+static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                               hipEvent_t e0, hipEvent_t e1, Args... args) {
+    // With events, the start/stop timestamps ride on the dispatch packet
+    // itself (no extra barrier packets between kernels).
+    if (e0 && e1)
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, e0, e1, 0, args...);
     else
-        hipLaunchKernelGGL((k_blur<R, false>), grid, dim3(256), 0, s, src, dst, W, H, rows,
-                           taps, dec, Wd, Hd);
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
     return hipGetLastError();
 }
 
-using BlurFn = hipError_t (*)(const double*, double*, int, int, int, const BlurTaps&,
-                              double*, int, int, hipStream_t);
+template <int R, int MODE>
+static hipError_t launch_blur_r(const BlurSource& src, double* dst, int W, int H, int rows,
+                                const BlurTaps& taps, double* dec, int Wd, int Hd,
+                                hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    dim3 grid((W + 63) / 64, ((H + rows - 1) / rows + 3) / 4);
+    if (MODE == kSrcPlane && dec)
+        return launch_timed(k_blur<R, true, kSrcPlane>, grid, dim3(256), 0, s, e0, e1, src, dst,
+                            W, H, rows, taps, dec, Wd, Hd);
+    return launch_timed(k_blur<R, false, MODE>, grid, dim3(256), 0, s, e0, e1, src, dst, W, H,
+                        rows, taps, dec, Wd, Hd);
+}
 
-template <int... Rs>
+using BlurFn = hipError_t (*)(const BlurSource&, double*, int, int, int, const BlurTaps&,
+                              double*, int, int, hipStream_t, hipEvent_t, hipEvent_t);
+
+template <int MODE, int... Rs>
 struct BlurTable {
-    static constexpr BlurFn fns[sizeof...(Rs)] = {&launch_blur_r<Rs>...};
+    static constexpr BlurFn fns[sizeof...(Rs)] = {&launch_blur_r<Rs, MODE>...};
 };
-template <int... Rs>
-constexpr BlurFn BlurTable<Rs...>::fns[sizeof...(Rs)];
+template <int MODE, int... Rs>
+constexpr BlurFn BlurTable<MODE, Rs...>::fns[sizeof...(Rs)];
 
-using BlurAll = BlurTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
-static_assert(kMaxTemplR == 16, "BlurAll must cover 1..kMaxTemplR");
+#define SIFT_R_LIST 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16
+using BlurPlane = BlurTable<kSrcPlane, SIFT_R_LIST>;
+using BlurGray = BlurTable<kSrcGray, SIFT_R_LIST>;
+using BlurUps = BlurTable<kSrcUpsample, SIFT_R_LIST>;
+#undef SIFT_R_LIST
+static_assert(kMaxTemplR == 16, "blur tables must cover 1..kMaxTemplR");
 
 int blur_rows_for(int W, int H, int R) {
     // Strip height trades the 2R-row priming of every strip against the
@@ -866,18 +1016,40 @@ int blur_rows_for(int W, int H, int R) {
 }
 
 hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurTaps& taps,
-                       double* dec, int Wd, int Hd, double* tmp, hipStream_t s) {
+                       double* dec, int Wd, int Hd, double* tmp, hipStream_t s, hipEvent_t e0,
+                       hipEvent_t e1) {
     const int R = taps.R;
     if (R >= 1 && R <= kMaxTemplR) {
         const int rows = blur_rows_for(W, H, R);
-        return BlurAll::fns[R - 1](src, dst, W, H, rows, taps, dec, Wd, Hd, s);
+        const BlurSource bs{src, W, H, 1};
+        return BlurPlane::fns[R - 1](bs, dst, W, H, rows, taps, dec, Wd, Hd, s, e0, e1);
     }
     // wide kernels (or R == 0): generic two-pass path through `tmp`
     dim3 grid((W + 255) / 256, H);
+    if (e0) {
+        hipError_t e = hipEventRecord(e0, s);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_blur_rows_any, grid, dim3(256), 0, s, src, tmp, W, H, taps);
     hipLaunchKernelGGL(k_blur_cols_any, grid, dim3(256), 0, s, tmp, dst, W, H, taps, dec,
                        Wd, Hd);
+    if (e1) {
+        hipError_t e = hipEventRecord(e1, s);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
+}
+
+bool launch_blur_initial_fused(const double* in, int w, int h, int c, int dbl, double* dst,
+                               int W0, int H0, const BlurTaps& taps, hipStream_t s,
+                               hipEvent_t e0, hipEvent_t e1, hipError_t* err) {
+    const int R = taps.R;
+    if (R < 1 || R > kMaxTemplR || (c == 1 && !dbl)) return false;
+    const int rows = blur_rows_for(W0, H0, R);
+    const BlurSource bs{in, w, h, c};
+    *err = dbl ? BlurUps::fns[R - 1](bs, dst, W0, H0, rows, taps, nullptr, 0, 0, s, e0, e1)
+               : BlurGray::fns[R - 1](bs, dst, W0, H0, rows, taps, nullptr, 0, 0, s, e0, e1);
+    return true;
 }
 
 hipError_t prepare_kernel_attributes() {
@@ -887,11 +1059,10 @@ hipError_t prepare_kernel_attributes() {
 }
 
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
-                              const BlurTaps* d_taps, hipStream_t s) {
-    const size_t lds = kLdsOctaveBytes;
-    hipLaunchKernelGGL(k_octaves_lds, dim3(1), dim3(1024), lds, s, d_pt, o_first, o_last,
-                       n_gauss, d_taps);
-    return hipGetLastError();
+                              const BlurTaps* d_taps, hipStream_t s, hipEvent_t e0,
+                              hipEvent_t e1) {
+    return launch_timed(k_octaves_lds, dim3(1), dim3(1024), kLdsOctaveBytes, s, e0, e1, d_pt,
+                        o_first, o_last, n_gauss, d_taps);
 }
 
 hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double* out,
@@ -904,7 +1075,7 @@ hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double
 hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
                                 int thr, sift_extremum* out, unsigned* counter, unsigned cap,
                                 hipStream_t s) {
-    const int blocks = eg.first_tile[eg.octaves];
+    const int blocks = eg.first_tile[eg.n];
     if (blocks == 0) return hipSuccess;
     switch (n_gauss) {
 #define SIFT_EXT_CASE(NL)                                                                 \
@@ -937,37 +1108,50 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_g
     return hipGetLastError();
 }
 
-hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P,
-                         const sift_extremum* cand, const unsigned* n_cand, unsigned cap_cand,
+__global__ void k_snapshot(const unsigned* __restrict__ ctr, unsigned* __restrict__ snap) {
+    if (threadIdx.x < 4) snap[threadIdx.x] = ctr[threadIdx.x];
+}
+
+hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s) {
+    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(64), 0, s, ctr, snap);
+    return hipGetLastError();
+}
+
+hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
+                         const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s) {
     unsigned blocks = (cap_cand + 255) / 256;
     if (blocks > 1024) blocks = 1024;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(k_refine, dim3(blocks), dim3(256), 0, s, d_pt, P, cand, n_cand,
+    hipLaunchKernelGGL(k_refine, dim3(blocks), dim3(256), 0, s, d_pt, P, cand, cand_begin, n_cand,
                        cap_cand, out, n_out, cap_out);
     return hipGetLastError();
 }
 
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
-                         const unsigned* n_raw, unsigned cap_raw, sift_kp* out,
-                         double* out_off0, unsigned* n_out, unsigned cap_out,
+                         const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
+                         sift_kp* out, double* out_off0, unsigned* n_out, unsigned cap_out,
                          hipStream_t s) {
     unsigned blocks = (cap_raw + 3) / 4;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, n_raw, cap_raw,
-                       out, out_off0, n_out, cap_out);
+    if (P.num_bins > 64)
+        hipLaunchKernelGGL(k_orient<true>, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin,
+                           n_raw, cap_raw, out, out_off0, n_out, cap_out);
+    else
+        hipLaunchKernelGGL(k_orient<false>, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin,
+                           n_raw, cap_raw, out, out_off0, n_out, cap_out);
     return hipGetLastError();
 }
 
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
-                             const unsigned* n, unsigned cap, float* desc_f32,
-                             hipStream_t s) {
+                             const unsigned* rec_begin, const unsigned* n, unsigned cap,
+                             float* desc_f32, hipStream_t s) {
     unsigned blocks = (cap + 3) / 4;
     if (blocks > 4096) blocks = 4096;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(k_descriptor, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, n, cap,
-                       desc_f32);
+    hipLaunchKernelGGL(k_descriptor, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_begin, n,
+                       cap, desc_f32);
     return hipGetLastError();
 }
 

@@ -40,6 +40,13 @@ struct BlurTaps {
     int pad;
 };
 
+// What k_blur stages rows from: a W x H plane (p, with w = W), or the input
+// image (p = HWC doubles of w x h x c) for the fused initial blur.
+struct BlurSource {
+    const double* p;
+    int w, h, c;
+};
+
 // Device-resident table of pyramid level planes.
 struct PyrTable {
     double* lvl[kMaxOctaves][kMaxLevels];
@@ -47,11 +54,12 @@ struct PyrTable {
     int h[kMaxOctaves];
 };
 
-// Flattened tile grid of the all-octave extrema launch: octave o owns blocks
-// [first_tile[o], first_tile[o+1]), tiles_x[o] tiles of 64 centre columns per
-// row of 16 centre rows.
+// Flattened tile grid of one extrema launch over a set of octaves: entry i
+// (octave oct[i]) owns blocks [first_tile[i], first_tile[i+1]), tiles_x[i]
+// tiles of 64 centre columns per band of 16 centre rows.
 struct ExtremaGrid {
-    int octaves;
+    int n;
+    int oct[kMaxOctaves];
     int tiles_x[kMaxOctaves];
     int first_tile[kMaxOctaves + 1];
 };

@@ -16,13 +16,17 @@ def main(path, n_images=None):
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
         tot[r["Kernel_Name"]] += d
         cnt[r["Kernel_Name"]] += 1
-    starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_prepare")]
-    n_img = n_images or len(starts)
+    # one counter memset (fillBuffer) opens every detect
+    starts = [i for i, r in enumerate(rows) if "fillBuffer" in r["Kernel_Name"]]
+    n_img = n_images or max(1, len(starts))
     print(f"{'kernel':40s} {'calls':>6s} {'total us':>10s} {'avg us':>9s} {'us/image':>9s}")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"{k[:40]:40s} {cnt[k]:6d} {v:10.1f} {v / cnt[k]:9.2f} {v / n_img:9.1f}")
     if len(starts) >= 2:
         a, b = starts[-2], starts[-1]
+        # the image's first pyramid launch precedes its memset by a few dispatches
+        a = max(0, a - 2)
+        b = max(a + 1, b - 2)
         seg = rows[a:b]
         t0 = int(seg[0]["Start_Timestamp"])
         t1 = int(rows[b]["Start_Timestamp"])
@@ -31,7 +35,9 @@ def main(path, n_images=None):
               f"span to next image {(t1 - t0) / 1000.0:.1f} us")
         for r in seg:
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
-            print(f"  {r['Kernel_Name'][:30]:30s} {d:8.1f} us  grid {r['Grid_Size_X']}x{r['Grid_Size_Y']}")
+            st = (int(r["Start_Timestamp"]) - t0) / 1000.0
+            print(f"  {r['Kernel_Name'][:30]:30s} start {st:8.1f} dur {d:8.1f} us  grid "
+                  f"{r['Grid_Size_X']}x{r['Grid_Size_Y']}")
 
 
 if __name__ == "__main__":
