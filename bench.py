@@ -82,6 +82,8 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true",
+                    help="skip the per-launch HIP events of the pyramid roofline")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "blur_traffic.json"),
                     help="PMC-derived HBM bytes per blur launch (rocprofv3 --pmc summary)")
     args = ap.parse_args()
@@ -129,7 +131,7 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ctx.set_profiling(True)
+    ctx.set_profiling(not args.no_events)
     ctx.blur_profile(reset=True)
     t0 = time.perf_counter()
     kp_total = 0

@@ -8,7 +8,7 @@
 // (image.cpp:226-235), the final keypoint size (std::pow, sift.cpp:427-429)
 // and clean_keypoints (std::sort + std::unique, sift.cpp:20-24). Everything
 // per-pixel and per-keypoint runs in the HIP kernels of sift_kernels.hip,
-// enqueued on one stream with no host synchronisation until the counters are
+// enqueued on three streams with no host synchronisation until the counters are
 // read back at the end.
 #include <hip/hip_runtime.h>
 
@@ -28,8 +28,13 @@ using namespace sift_amd;
 namespace {
 
 // device counter block: [0..3] live counters (candidates, refined, oriented),
-// [4..7] batch-0 begin (zeros), [8..11] batch-1 begin (snapshot)
-constexpr int kCtrWords = 12;
+// [4..7] zeros, then per keypoint batch g a 4-word snapshot taken after its
+// extrema (the batch's candidate end and its record begins), then two
+// keypoint work counters per chain (orientation, descriptor)
+constexpr int kCtrZeros = 4;
+constexpr int kCtrSnap = 8;
+constexpr int kCtrWork = kCtrSnap + 4 * (kMaxOctaves + 1);
+constexpr int kCtrWords = kCtrWork + 2 * (kMaxOctaves + 2);
 
 template <class T>
 struct Pinned {  // grow-only pinned host buffer (fast async D2H, no staging)
@@ -57,6 +62,35 @@ struct Stage {
     BlurTaps taps[kMaxLevels];
 };
 
+// Grow-only mapped, coherent pinned host buffer: kernels write it directly
+// (visible to the host once the writing kernel has completed).
+template <class T>
+struct Mapped {
+    T* h = nullptr;
+    T* d = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (h && cap >= n) return SIFT_OK;
+        release();
+        if (hipHostMalloc(&h, n * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess) {
+            h = nullptr;
+            return SIFT_ERR_NOMEM;
+        }
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0) != hipSuccess) {
+            release();
+            return SIFT_ERR_HIP;
+        }
+        cap = n;
+        return SIFT_OK;
+    }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        h = d = nullptr;
+        cap = 0;
+    }
+};
+
 struct EventPair {
     hipEvent_t a, b;
     double bytes;
@@ -67,7 +101,8 @@ struct EventPair {
 struct sift_ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // A: pyramid
-    hipStream_t stream2 = nullptr;  // B: extrema, refine, orientation, descriptor
+    hipStream_t stream2 = nullptr;  // B: odd octaves of the pyramid
+    hipStream_t stream3 = nullptr;  // C: extrema, refine, orientation, descriptor
     std::vector<hipEvent_t> sync_ev;
 
     double* d_in = nullptr;
@@ -105,6 +140,13 @@ struct sift_ctx {
     double prof_ms = 0.0;
     int64_t prof_launches = 0;
     double prof_bytes = 0.0;
+
+    // records exported by k_descriptor per keypoint batch (mapped pinned)
+    Mapped<sift_kp> exp_rec;
+    Mapped<double> exp_off0;
+    Mapped<unsigned> exp_cnt;  // [begin, end) per chain
+    std::vector<hipEvent_t> chain_ev;
+    std::vector<unsigned> run_start;
 
     // host staging (pinned)
     Pinned<sift_kp> h_ori;
@@ -169,7 +211,7 @@ int prof_events(sift_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1, double bytes) {
     return SIFT_OK;
 }
 
-int blur_launch(sift_ctx* ctx, const double* src, double* dst, int W, int H,
+int blur_launch(sift_ctx* ctx, hipStream_t s, const double* src, double* dst, int W, int H,
                 const BlurTaps& t, double* dec, int Wd, int Hd) {
     if (t.R > kMaxTemplR || t.R < 1) {
         if (ensure(&ctx->d_tmp, &ctx->tmp_cap, (size_t)W * H) != SIFT_OK) return SIFT_ERR_NOMEM;
@@ -177,7 +219,7 @@ int blur_launch(sift_ctx* ctx, const double* src, double* dst, int W, int H,
     hipEvent_t e0, e1;
     const double bytes = 16.0 * (double)W * (double)H + (dec ? 8.0 * (double)Wd * Hd : 0.0);
     if (prof_events(ctx, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
-    SIFT_HIP_TRY(launch_blur(src, dst, W, H, t, dec, Wd, Hd, ctx->d_tmp, ctx->stream, e0, e1));
+    SIFT_HIP_TRY(launch_blur(src, dst, W, H, t, dec, Wd, Hd, ctx->d_tmp, s, e0, e1));
     return SIFT_OK;
 }
 
@@ -248,15 +290,17 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         (st = ensure_t(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
         return st;
 
-    // Two streams: A (ctx->stream) builds the pyramid; B (ctx->stream2) runs
-    // the extrema of every octave as soon as that octave is complete (event
-    // per octave), then the small octaves' extrema after the LDS-resident
-    // kernel, then refine -> orientation -> descriptor. The octave-0 extrema
-    // overlap the octave-1..k blurs, and the single-CU small-octave kernel
-    // overlaps the big octaves' extrema.
-    hipStream_t sA = ctx->stream, sB = ctx->stream2;
+    // Three streams (HIP's default is four hardware queues per process, and
+    // streams beyond that share a queue and serialise): A (ctx->stream) and
+    // B (ctx->stream2) build the pyramid, even and odd octaves, at high
+    // priority; C (ctx->stream3) runs, per octave batch as soon as its levels
+    // exist, the extrema then refine -> orientation -> descriptor. The
+    // keypoint work of octave 0 overlaps the pyramid of the smaller octaves,
+    // which is latency-bound and leaves most of the chip idle.
+    hipStream_t sA = ctx->stream, sB = ctx->stream2, sC = ctx->stream3;
     int ev_i = 0;
 
+    SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sA));
     // ---- Gaussian pyramid (compute_initial_image + compute_gaussian_images)
     const int W0 = g.W[0], H0 = g.H[0];
     double* G00 = ctx->h_pt.lvl[0][0];
@@ -279,7 +323,8 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
                                             scratch, W0, H0, sA));
                 base_src = scratch;
             }
-            if ((st = blur_launch(ctx, base_src, G00, W0, H0, taps_init, nullptr, 0, 0)) != SIFT_OK)
+            if ((st = blur_launch(ctx, sA, base_src, G00, W0, H0, taps_init, nullptr, 0, 0)) !=
+                SIFT_OK)
                 return st;
         }
     }
@@ -293,44 +338,100 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             break;
         }
     const bool tiles = p->window_size / 2 == 1;
-    SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sB));
-    // refine -> orientation -> descriptor over the records appended since
-    // the counter snapshot `begin` (batch ranges, see launch_refine)
-    auto run_batch = [&](const unsigned* begin) -> int {
-        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, begin + 0, ctx->d_ctr + 0,
-                                   ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, sB));
-        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, begin + 1, ctx->d_ctr + 1,
-                                   ctx->cap_raw, ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2,
-                                   ctx->cap_ori, sB));
-        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, begin + 2, ctx->d_ctr + 2,
-                                       ctx->cap_ori, out_desc_f32 ? ctx->d_df32 : nullptr, sB));
+    // Keypoint batches, one per large octave plus one for the LDS-resident
+    // small octaves, all on stream C: extrema of the batch's octaves, a
+    // snapshot of the counters (the batch's candidate end and its record
+    // begins), then refine over [previous end, this end) -> orientation ->
+    // descriptor over the records appended since the snapshot.
+    const unsigned* zeros = ctx->d_ctr + kCtrZeros;
+    auto snap = [&](int g) { return ctx->d_ctr + kCtrSnap + 4 * g; };
+    auto launch_extrema_range = [&](int o_begin, int o_end) -> int {
+        if (tiles) {
+            const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
+            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
+                                              ctx->d_ctr + 0, ctx->cap_cand, sC));
+        } else {
+            for (int o = o_begin; o < o_end; ++o)
+                SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
+                                                p->window_size, dp.threshold, ctx->d_cand,
+                                                ctx->d_ctr + 0, ctx->cap_cand, sC));
+        }
         return SIFT_OK;
     };
-    const unsigned* batch0 = ctx->d_ctr + 4;
-    unsigned* batch1 = ctx->d_ctr + 8;
+    // refine -> orientation -> descriptor over candidates [cand_begin,
+    // cand_end) and the records they append (ranges from counter snapshots)
+    // records of every chain also go to the mapped export buffers, sized from
+    // the largest record count seen so far (a larger one falls back to one
+    // bulk download at the end, and grows them for the next call)
+    if ((st = ctx->exp_rec.ensure(std::max<size_t>(ctx->exp_rec.cap, 16384))) != SIFT_OK ||
+        (st = ctx->exp_off0.ensure(ctx->exp_rec.cap)) != SIFT_OK ||
+        (st = ctx->exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
+        return st;
+    int n_chains = 0;
+    auto run_chain = [&](const unsigned* cand_begin, const unsigned* cand_end,
+                         const unsigned* begin, hipStream_t sx) -> int {
+        const int ci = n_chains++;
+        unsigned* work = ctx->d_ctr + kCtrWork + 2 * ci;
+        while ((int)ctx->chain_ev.size() <= ci) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                return SIFT_ERR_HIP;
+            ctx->chain_ev.push_back(e);
+        }
+        const ExportSink ex{ctx->exp_rec.d, ctx->exp_off0.d, ctx->exp_cnt.d + 2 * ci, ctx->d_off0,
+                            (unsigned)ctx->exp_rec.cap};
+        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin, cand_end,
+                                   ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, sx));
+        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, begin + 1, ctx->d_ctr + 1,
+                                   ctx->cap_raw, ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2,
+                                   ctx->cap_ori, work, sx));
+        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, begin + 2, ctx->d_ctr + 2,
+                                       ctx->cap_ori, out_desc_f32 ? ctx->d_df32 : nullptr,
+                                       work + 1, ex, sx));
+        SIFT_HIP_TRY(hipEventRecord(ctx->chain_ev[ci], sx));
+        return SIFT_OK;
+    };
+    int n_batches = 0;
+    // batch g: octaves [o_begin, o_end), whose last level was enqueued on sp
+    auto batch = [&](int o_begin, int o_end, hipStream_t sp) -> int {
+        const int gb = n_batches++;
+        hipEvent_t pyr_done = sync_event(ctx, ev_i++);
+        if (!pyr_done) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
+        SIFT_HIP_TRY(hipStreamWaitEvent(sC, pyr_done, 0));
+        int st2 = launch_extrema_range(o_begin, o_end);
+        if (st2 != SIFT_OK) return st2;
+        SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, snap(gb), sC));
+        return run_chain(gb == 0 ? zeros : snap(gb - 1), snap(gb), snap(gb), sC);
+    };
+    // The pyramid alternates between two streams, octave o on pyr[o % 2]:
+    // octave o+1 only needs the decimated level `intervals` of octave o, so it
+    // starts as soon as that level exists and overlaps the last two levels of
+    // octave o (the small octaves are latency-bound: two in flight at once).
+    hipStream_t pyr[2] = {sA, sB};
+    hipEvent_t base_ready = nullptr;  // next octave's base written (decimation)
+    auto next_base_event = [&](hipStream_t so) -> int {
+        base_ready = sync_event(ctx, ev_i++);
+        if (!base_ready) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(hipEventRecord(base_ready, so));
+        return SIFT_OK;
+    };
     for (int o = 0; o < o_small; ++o) {
+        hipStream_t so = pyr[o & 1];
+        if (o > 0) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
         for (int l = 1; l < g.n_gauss; ++l) {
             const bool dec = (l == dec_level) && (o + 1 < g.octaves);
-            st = blur_launch(ctx, ctx->h_pt.lvl[o][l - 1], ctx->h_pt.lvl[o][l], g.W[o], g.H[o],
-                             taps[l], dec ? ctx->h_pt.lvl[o + 1][0] : nullptr,
+            st = blur_launch(ctx, so, ctx->h_pt.lvl[o][l - 1], ctx->h_pt.lvl[o][l], g.W[o],
+                             g.H[o], taps[l], dec ? ctx->h_pt.lvl[o + 1][0] : nullptr,
                              dec ? g.W[o + 1] : 0, dec ? g.H[o + 1] : 0);
             if (st != SIFT_OK) return st;
+            if (dec && (st = next_base_event(so)) != SIFT_OK) return st;
         }
-        hipEvent_t done = sync_event(ctx, ev_i++);
-        if (!done) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(done, sA));
-        SIFT_HIP_TRY(hipStreamWaitEvent(sB, done, 0));
-        if (tiles) {
-            const ExtremaGrid eg = extrema_grid(g, o, o + 1);
-            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
-                                              ctx->d_ctr + 0, ctx->cap_cand, sB));
-        } else {
-            SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
-                                            p->window_size, dp.threshold, ctx->d_cand,
-                                            ctx->d_ctr + 0, ctx->cap_cand, sB));
-        }
+        if ((st = batch(o, o + 1, so)) != SIFT_OK) return st;
     }
     if (o_small < g.octaves) {
+        hipStream_t so = pyr[o_small & 1];
+        if (o_small > 0) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
         double bytes = 0.0;
         for (int o = o_small; o < g.octaves; ++o) {
             bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[o] * (double)g.H[o];
@@ -339,53 +440,54 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         hipEvent_t e0, e1;
         if (prof_events(ctx, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(ctx->d_pt, o_small, g.octaves - 1, g.n_gauss,
-                                        ctx->d_taps, sA, e0, e1));
+                                        ctx->d_taps, so, e0, e1));
+        if ((st = batch(o_small, g.octaves, so)) != SIFT_OK) return st;
     }
-    // batch 0: keypoints of the large octaves, while stream A still runs the
-    // single-workgroup small-octave kernel
-    if (o_small > 0 && (st = run_batch(batch0)) != SIFT_OK) return st;
-    if (o_small < g.octaves) {
-        // batch 1: the small octaves, from a snapshot of the counters
-        SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, batch1, sB));
-        hipEvent_t done = sync_event(ctx, ev_i++);
-        if (!done) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(done, sA));
-        SIFT_HIP_TRY(hipStreamWaitEvent(sB, done, 0));
-        if (tiles) {
-            const ExtremaGrid eg = extrema_grid(g, o_small, g.octaves);
-            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
-                                              ctx->d_ctr + 0, ctx->cap_cand, sB));
-        } else {
-            for (int o = o_small; o < g.octaves; ++o)
-                SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
-                                                p->window_size, dp.threshold, ctx->d_cand,
-                                                ctx->d_ctr + 0, ctx->cap_cand, sB));
-        }
-        if ((st = run_batch(batch1)) != SIFT_OK) return st;
+    // stream B joins A (the ctx's public stream) before the call returns
+    {
+        hipEvent_t j = sync_event(ctx, ev_i++);
+        if (!j) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(hipEventRecord(j, sB));
+        SIFT_HIP_TRY(hipStreamWaitEvent(sA, j, 0));
     }
 
-    // ---- wait for the counters; re-run every candidate stage on overflow
-    clk::time_point t_enq, t_wait;
-    for (int attempt = 0;; ++attempt) {
-        if (attempt > 0) {  // pyramid is complete; one batch over everything
-            SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sB));
-            if (tiles) {
-                const ExtremaGrid eg = extrema_grid(g, 0, g.octaves);
-                SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold,
-                                                  ctx->d_cand, ctx->d_ctr + 0, ctx->cap_cand,
-                                                  sB));
-            } else {
-                for (int o = 0; o < g.octaves; ++o)
-                    SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
-                                                    p->window_size, dp.threshold, ctx->d_cand,
-                                                    ctx->d_ctr + 0, ctx->cap_cand, sB));
-            }
-            if ((st = run_batch(batch0)) != SIFT_OK) return st;
+    // ---- finalise each batch on the host while the device runs the next:
+    // sizes with glibc pow and a sorted run per batch, from the exported
+    // records (sift.cpp:20-24, 427-429)
+    SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
+                                hipMemcpyDeviceToHost, sC));
+    clk::time_point t_enq = clk::now(), t_wait;
+    bool exported = true;
+    unsigned n_keys = 0;
+    ctx->run_start.clear();
+    ctx->fin_ws.all.resize(ctx->exp_rec.cap);
+    for (int ci = 0; ci < n_chains; ++ci) {
+        SIFT_HIP_TRY(hipEventSynchronize(ctx->chain_ev[ci]));
+        const unsigned b = ctx->exp_cnt.h[2 * ci], e = ctx->exp_cnt.h[2 * ci + 1];
+        if (e > ctx->exp_rec.cap || b > e) {
+            exported = false;
+            break;
         }
-        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
-                                    hipMemcpyDeviceToHost, sB));
-        t_enq = clk::now();
-        SIFT_HIP_TRY(hipStreamSynchronize(sB));
+        host_sizes(p, ctx->exp_rec.h, ctx->exp_off0.h, b, e);
+        ctx->run_start.push_back(n_keys);
+        host_sort_run(ctx->exp_rec.h, b, e, ctx->fin_ws.all.data() + n_keys, &ctx->fin_ws);
+        n_keys += e - b;
+    }
+    ctx->run_start.push_back(n_keys);
+
+    // ---- the counters; re-run every candidate stage on overflow
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 0) {  // pyramid is complete; one batch over everything, on C
+            exported = false;
+            SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
+            SIFT_HIP_TRY(hipStreamSynchronize(sC));
+            if ((st = launch_extrema_range(0, g.octaves)) != SIFT_OK) return st;
+            n_chains = 0;
+            if ((st = run_chain(zeros, ctx->d_ctr + 0, zeros, sC)) != SIFT_OK) return st;
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
+                                        hipMemcpyDeviceToHost, sC));
+        }
+        SIFT_HIP_TRY(hipStreamSynchronize(sC));
         t_wait = clk::now();
         const unsigned nc = ctx->h_ctr[0], nr = ctx->h_ctr[1], no = ctx->h_ctr[2];
         if (nc <= ctx->cap_cand && nr <= ctx->cap_raw && no <= ctx->cap_ori) break;
@@ -405,22 +507,27 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     }
 
     const unsigned n_ori = ctx->h_ctr[2];
-    if ((st = ctx->h_ori.ensure(n_ori)) != SIFT_OK) return st;
-    if ((st = ctx->h_off0.ensure(n_ori)) != SIFT_OK) return st;
-    if (n_ori) {
-        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.p, ctx->d_ori, n_ori * sizeof(sift_kp),
-                                    hipMemcpyDeviceToHost, ctx->stream2));
-        SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.p, ctx->d_off0, n_ori * sizeof(double),
-                                    hipMemcpyDeviceToHost, ctx->stream2));
+    if (exported && n_keys != n_ori) exported = false;
+    const sift_kp* rec_src = ctx->exp_rec.h;
+    if (!exported) {  // bulk download of every record
+        if ((st = ctx->h_ori.ensure(n_ori)) != SIFT_OK) return st;
+        if ((st = ctx->h_off0.ensure(n_ori)) != SIFT_OK) return st;
+        if (n_ori) {
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.p, ctx->d_ori, n_ori * sizeof(sift_kp),
+                                        hipMemcpyDeviceToHost, sC));
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.p, ctx->d_off0, n_ori * sizeof(double),
+                                        hipMemcpyDeviceToHost, sC));
+        }
+        rec_src = ctx->h_ori.p;
     }
     if (out_desc_f32) {
         if ((st = ctx->h_df32.ensure((size_t)n_ori * 128)) != SIFT_OK) return st;
         if (n_ori)
             SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.p, ctx->d_df32,
                                         (size_t)n_ori * 128 * sizeof(float),
-                                        hipMemcpyDeviceToHost, ctx->stream2));
+                                        hipMemcpyDeviceToHost, sC));
     }
-    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    SIFT_HIP_TRY(hipStreamSynchronize(sC));
     const auto t_copy = clk::now();
 
     if (ctx->profiling) {
@@ -434,15 +541,29 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         ctx->pending.clear();
     }
 
-    // final size with glibc pow + clean_keypoints, in the g++-built layer
+    // clean_keypoints: merge the sorted runs and unique (or all of it, after
+    // a bulk download), in the g++-built layer
     ctx->keep.resize(n_ori);
-    const size_t n = host_finalize(p, ctx->h_ori.p, ctx->h_off0.p, n_ori, ctx->keep.data(),
-                                   &ctx->fin_ws);
+    size_t n;
+    if (exported) {
+        n = host_merge_unique(ctx->exp_rec.h, ctx->fin_ws.all.data(), ctx->run_start,
+                              ctx->keep.data(), &ctx->fin_ws);
+    } else {
+        n = host_finalize(p, ctx->h_ori.p, ctx->h_off0.p, n_ori, ctx->keep.data(),
+                          &ctx->fin_ws);
+        // the next call exports this many records
+        if (n_ori > ctx->exp_rec.cap) {
+            const size_t want = (size_t)n_ori + n_ori / 2;
+            if ((st = ctx->exp_rec.ensure(want)) != SIFT_OK ||
+                (st = ctx->exp_off0.ensure(want)) != SIFT_OK)
+                return st;
+        }
+    }
     const auto t_fin = clk::now();
 
     sift_kp* kps = (sift_kp*)std::malloc(std::max<size_t>(n, 1) * sizeof(sift_kp));
     if (!kps) return SIFT_ERR_NOMEM;
-    for (size_t i = 0; i < n; ++i) kps[i] = ctx->h_ori.p[ctx->keep[i]];
+    for (size_t i = 0; i < n; ++i) kps[i] = rec_src[ctx->keep[i]];
     float* df = nullptr;
     if (out_desc_f32) {
         df = (float*)std::malloc(std::max<size_t>(n, 1) * 128 * sizeof(float));
@@ -508,8 +629,11 @@ int sift_hip_create(int device, sift_ctx** out) {
     sift_ctx* ctx = new (std::nothrow) sift_ctx();
     if (!ctx) return SIFT_ERR_NOMEM;
     ctx->device = device;
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+    int prio_lo = 0, prio_hi = 0;  // numerically lower = higher priority
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+    if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess ||
         hipMalloc(&ctx->d_ctr, kCtrWords * sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&ctx->h_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&ctx->h_stage, sizeof(Stage)) != hipSuccess ||
@@ -529,6 +653,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+    if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
     void* bufs[] = {ctx->d_in, ctx->d_pyr, ctx->d_tmp, ctx->d_cand, ctx->d_raw,
                     ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_stage};
     for (void* b : bufs)
@@ -536,12 +661,17 @@ int sift_hip_destroy(sift_ctx* ctx) {
     if (ctx->h_ctr) (void)hipHostFree(ctx->h_ctr);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     ctx->h_ori.release();
+    ctx->exp_rec.release();
+    ctx->exp_off0.release();
+    ctx->exp_cnt.release();
+    for (hipEvent_t e : ctx->chain_ev) (void)hipEventDestroy(e);
     ctx->h_off0.release();
     ctx->h_df32.release();
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
     delete ctx;
     return SIFT_OK;
 }

@@ -26,6 +26,9 @@ bool make_taps(double sigma, BlurTaps* t) {
     double s = t->k[0];
     for (int u = 1; u < ks; ++u) s += 2.0 * t->k[u];
     t->sum_w = s;
+    // RN(1/sum_w): the kernels divide by sum_w with Markstein's correction
+    // (q = a*inv; r = fma(-q, sum_w, a); q + r*inv), correctly rounded
+    t->inv = 1.0 / s;
     t->R = ks - 1;
     return true;
 }
@@ -106,9 +109,9 @@ int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* 
     return SIFT_OK;
 }
 
-size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
-                     unsigned* keep, FinalizeWorkspace* ws) {
-    for (unsigned i = 0; i < n; ++i) {
+void host_sizes(const sift_params* p, sift_kp* recs, const double* off0, unsigned b,
+                unsigned e) {
+    for (unsigned i = b; i < e; ++i) {
         sift_kp& r = recs[i];
         // std::pow(2, octave) is exactly 2^octave; ldexp gives the same value
         const double scale = std::ldexp(1.0, r.octave);
@@ -117,29 +120,38 @@ size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, un
         if (p->double_image_size) size /= 2;
         r.size = size;
     }
+}
+
+namespace {
+
+// Keypoint::operator< (sift.hh:31-41): x asc, y asc, size desc, pori asc,
+// octave desc
+bool key_less(const FinalizeKey& a, const FinalizeKey& b) {
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.pori != b.pori) return a.pori < b.pori;
+    return a.octave > b.octave;
+}
+
+}  // namespace
+
+void host_sort_run(const sift_kp* recs, unsigned b, unsigned e, FinalizeKey* out,
+                   FinalizeWorkspace* ws) {
     // Sort a compact key array (40 B per record) in Keypoint::operator<
-    // order (sift.hh:31-41: x asc, y asc, size desc, pori asc, octave desc).
-    // x >= 0 for every keypoint, and b(x) = x / x_max * B is monotone
-    // non-decreasing under round-to-nearest, so a stable bucket pass on b(x)
-    // followed by a comparator sort inside each (tiny) bucket yields exactly
-    // the order std::sort with the full comparator would, in O(n + B).
+    // order. x >= 0 for every keypoint, and bucket(x) = x / x_max * B is
+    // monotone non-decreasing under round-to-nearest, so a stable bucket
+    // pass followed by a comparator sort inside each (tiny) bucket yields
+    // exactly the order std::sort with the full comparator would, in O(n + B).
     using Key = FinalizeKey;
-    auto less = [](const Key& a, const Key& b) {
-        if (a.x != b.x) return a.x < b.x;
-        if (a.y != b.y) return a.y < b.y;
-        if (a.size != b.size) return a.size > b.size;
-        if (a.pori != b.pori) return a.pori < b.pori;
-        return a.octave > b.octave;
-    };
-    // workspace reused across calls (no per-call allocation / page faults)
+    const unsigned n = e - b;
     std::vector<Key>& keys = ws->keys;
-    std::vector<Key>& sorted = ws->sorted;
     keys.resize(n);
-    sorted.resize(n);
     double x_max = 0.0;
     for (unsigned i = 0; i < n; ++i) {
-        keys[i] = {recs[i].x, recs[i].y, recs[i].size, recs[i].pori, recs[i].octave, i};
-        x_max = std::max(x_max, recs[i].x);
+        const sift_kp& r = recs[b + i];
+        keys[i] = {r.x, r.y, r.size, r.pori, r.octave, b + i};
+        x_max = std::max(x_max, r.x);
     }
     const size_t B = std::max<size_t>(1, std::min<size_t>(n, (size_t)1 << 20));
     std::vector<unsigned>& start = ws->start;
@@ -150,20 +162,48 @@ size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, un
         return f >= (double)(B - 1) ? B - 1 : (f <= 0.0 ? 0 : (size_t)f);
     };
     for (unsigned i = 0; i < n; ++i) ++start[bucket(keys[i].x) + 1];
-    for (size_t b = 0; b < B; ++b) start[b + 1] += start[b];
+    for (size_t q = 0; q < B; ++q) start[q + 1] += start[q];
     {
         std::vector<unsigned>& fill = ws->fill;
         fill.assign(start.begin(), start.end() - 1);
-        for (unsigned i = 0; i < n; ++i) sorted[fill[bucket(keys[i].x)]++] = keys[i];
+        for (unsigned i = 0; i < n; ++i) out[fill[bucket(keys[i].x)]++] = keys[i];
     }
-    for (size_t b = 0; b < B; ++b) {
-        Key* lo = sorted.data() + start[b];
-        Key* hi = sorted.data() + start[b + 1];
-        if (hi - lo > 1) std::sort(lo, hi, less);
+    for (size_t q = 0; q < B; ++q) {
+        Key* lo = out + start[q];
+        Key* hi = out + start[q + 1];
+        if (hi - lo > 1) std::sort(lo, hi, key_less);
+    }
+}
+
+size_t host_merge_unique(const sift_kp* recs, FinalizeKey* keys,
+                         const std::vector<unsigned>& run_start, unsigned* keep,
+                         FinalizeWorkspace* ws) {
+    // pairwise merges of the sorted runs [run_start[i], run_start[i+1])
+    std::vector<unsigned> bounds(run_start);
+    const unsigned n = bounds.empty() ? 0 : bounds.back();
+    std::vector<FinalizeKey>& tmp = ws->sorted;
+    tmp.resize(n);
+    FinalizeKey* src = keys;
+    FinalizeKey* dst = tmp.data();
+    while (bounds.size() > 2) {
+        std::vector<unsigned> nb;
+        nb.push_back(0);
+        size_t i = 0;
+        for (; i + 2 < bounds.size(); i += 2) {
+            std::merge(src + bounds[i], src + bounds[i + 1], src + bounds[i + 1],
+                       src + bounds[i + 2], dst + bounds[i], key_less);
+            nb.push_back(bounds[i + 2]);
+        }
+        if (i + 1 < bounds.size()) {  // odd run out: carried over
+            std::copy(src + bounds[i], src + bounds[i + 1], dst + bounds[i]);
+            nb.push_back(bounds[i + 1]);
+        }
+        bounds.swap(nb);
+        std::swap(src, dst);
     }
     size_t m = 0;
     for (unsigned i = 0; i < n; ++i) {
-        const Key& k = sorted[i];
+        const FinalizeKey& k = src[i];
         if (m > 0) {
             // std::unique compares with the last kept element (Keypoint::
             // operator==, sift.hh:25-27: x, y, size, pori)
@@ -174,6 +214,14 @@ size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, un
         keep[m++] = k.idx;
     }
     return m;
+}
+
+size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
+                     unsigned* keep, FinalizeWorkspace* ws) {
+    host_sizes(p, recs, off0, 0, n);
+    ws->all.resize(n);
+    host_sort_run(recs, 0, n, ws->all.data(), ws);
+    return host_merge_unique(recs, ws->all.data(), {0u, n}, keep, ws);
 }
 
 }  // namespace sift_amd

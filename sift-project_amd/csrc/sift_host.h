@@ -30,18 +30,31 @@ int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* 
               BlurTaps* taps, DevParams* dp);
 
 // Final keypoint size with glibc pow (sift.cpp:427-429, halved at
-// sift.cpp:525) written into recs[i].size, then clean_keypoints
-// (sift.cpp:20-24): indices of the sorted, de-duplicated records go to keep[]
-// (capacity n). Returns the number kept.
+// sift.cpp:525) written into recs[i].size for i in [b, e).
+void host_sizes(const sift_params* p, sift_kp* recs, const double* off0, unsigned b,
+                unsigned e);
+
+// clean_keypoints (sift.cpp:20-24) in pieces, so a detect can sort the
+// records of each keypoint batch while the device still works on the next:
+// host_sort_run sorts the keys of records [b, e) (Keypoint::operator<,
+// sift.hh:31-41) into out[0, e-b); host_merge_unique merges consecutive
+// sorted runs of `keys` (boundaries run_start, last = total) and applies
+// std::unique (sift.hh:25-27), writing the kept record indices to keep[].
 struct FinalizeKey {
     double x, y, size, pori;
     int octave;
     unsigned idx;
 };
 struct FinalizeWorkspace {  // reused across calls
-    std::vector<FinalizeKey> keys, sorted;
+    std::vector<FinalizeKey> keys, sorted, all;
     std::vector<unsigned> start, fill;
 };
+void host_sort_run(const sift_kp* recs, unsigned b, unsigned e, FinalizeKey* out,
+                   FinalizeWorkspace* ws);
+size_t host_merge_unique(const sift_kp* recs, FinalizeKey* keys,
+                         const std::vector<unsigned>& run_start, unsigned* keep,
+                         FinalizeWorkspace* ws);
+// all of it over records [0, n): sizes, one run, merge/unique
 size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
                      unsigned* keep, FinalizeWorkspace* ws);
 

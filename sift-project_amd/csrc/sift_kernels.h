@@ -10,7 +10,11 @@
 
 namespace sift_amd {
 
-int blur_rows_for(int W, int H, int R);
+struct BlurShape {
+    int cols;  // adjacent columns per lane (strip width 64*cols)
+    int rows;  // output rows per wavefront strip
+};
+BlurShape blur_shape_for(int W, int H, int R);
 hipError_t prepare_kernel_attributes();
 
 hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double* out,
@@ -42,9 +46,11 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* out, double* out_off0, unsigned* n_out, unsigned cap_out,
-                         hipStream_t s);
+                         unsigned* work, hipStream_t s);
+// `work`: a zeroed device word, the keypoint work counter of this launch
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
                              const unsigned* rec_begin, const unsigned* n, unsigned cap,
-                             float* desc_f32, hipStream_t s);
+                             float* desc_f32, unsigned* work, const ExportSink& ex,
+                             hipStream_t s);
 
 }  // namespace sift_amd

@@ -41,6 +41,12 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) {
 // 2^e for small integer e, exact (the reference uses std::pow(2, int)).
 __device__ __forceinline__ double pow2i(int e) { return ldexp(1.0, e); }
 
+// Pyramid planes are device (global) memory; pointers read from the PyrTable
+// are generic to the compiler, which would emit flat loads (counted in both
+// vmcnt and lgkmcnt). Viewing them in address space 1 gives global loads.
+typedef __attribute__((address_space(1))) const double gdouble;
+__device__ __forceinline__ gdouble* gbl(const double* p) { return (gdouble*)p; }
+
 // XCD-aware block remap (bijective): workgroups are dealt round-robin over
 // the 8 XCDs, so consecutive block ids land on different L2s. Renumber so
 // every XCD owns one contiguous range of logical tiles; neighbouring strips
@@ -112,92 +118,153 @@ __global__ __launch_bounds__(256) void k_prepare(const double* __restrict__ in, 
     out[(size_t)oy * W0 + ox] = v0 * (1 - dy) + v1 * dy;
 }
 
+// Correctly rounded a / s for the per-kernel constant s = sum_w, with
+// inv = RN(1/s) from the host: q = RN(a*inv) is faithful and Markstein's
+// correction q + (a - q*s)*inv (residual exact by FMA) rounds to RN(a/s) —
+// the same final step as gfx950's own v_div_fmas sequence, without the
+// v_rcp_f64 / Newton / scaling part. Checked against IEEE division on
+// 2.5e12 random operands over every divisor the default pyramids use
+// (tools/blur_lab.hip divcheck, 0 mismatches); the pyramid parity tests
+// compare every level bit for bit.
+__device__ __forceinline__ double div_sum_w(double a, double s, double inv) {
+    const double q = a * inv;
+    const double r = __builtin_fma(-q, s, a);
+    return __builtin_fma(r, inv, q);
+}
+
 // ---------------------------------------------------------------------------
-// k_blur<R>: apply_gaussian_blur_fast / apply_double_convolution_1d
+// k_blur<R, C>: apply_gaussian_blur_fast / apply_double_convolution_1d
 // (image.cpp:156-238), both passes in one kernel.
 //
-// One wavefront owns a 64-column strip of `rows` output rows. It slides down
-// the strip one source row at a time: the row (plus an R-pixel replicate
-// halo each side) is staged in a per-wave LDS line, every lane computes the
-// horizontal pass for its column from LDS (2R+1 reads), and pushes the f64
-// result into a (2R+1)-deep register window; once primed, the vertical pass
-// runs entirely in registers. HBM traffic is one read of the source rows
-// (+2R/rows priming overlap, L2-served) and one write per output pixel.
-// Replicate borders: staged columns and source rows are clamped, which is
-// exactly the reference's min(x+u, W-1) / max(x-u, 0) (image.cpp:177-180,
-// 200-203). DECIM additionally writes resize_inter_nearest (image.cpp:41-55)
-// of the output, i.e. the next octave's base (sift.cpp:195-196).
+// One wavefront owns a strip of 64*C columns (C adjacent columns per lane)
+// and `rows` output rows, and slides down it one source row per step:
+//  * the source row (+R replicate halo each side) is staged in a per-wave
+//    LDS line, the next PF rows are already in flight in registers;
+//  * row pass of source row yy from LDS (C = 2: b128 reads of column pairs);
+//  * in the same step, the column pass of output row yy-R-1 from a
+//    (2R+2)-deep register window that does not include row yy — the two
+//    f64 dependency chains are independent, so their latencies overlap
+//    (measured: 20-30 % over computing the column pass of yy-R after the row
+//    pass of yy; tools/blur_lab.hip IL variants);
+//  * the window slot of every row is a compile-time constant (the step loop
+//    is unrolled by the window depth), so the window never moves.
+// Every lane issues every load and store (rows clamped; out-of-image
+// outputs go to a per-wave trash line). Replicate borders: staged columns and
+// source rows are clamped, i.e. the reference's min(x+u, W-1) / max(x-u, 0)
+// (image.cpp:177-180, 200-203). DECIM also writes resize_inter_nearest
+// (image.cpp:41-55) of the output, the next octave's base (sift.cpp:195-196).
+// HBM traffic: one read of the source rows (+2R/rows priming overlap, mostly
+// L2-served) and one write per output pixel.
 // ---------------------------------------------------------------------------
-template <int R, bool DECIM, int MODE>
+template <int R, int C, bool DECIM, int MODE>
 __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict__ dst, int W,
                                               int H, int rows, BlurTaps taps,
                                               double* __restrict__ dec, int Wd, int Hd) {
-    constexpr int NW = 2 * R + 1;  // register window depth
-    constexpr int SEG = 64 + 2 * R;
-    __shared__ double sline[4][SEG];
+    constexpr int PF = 2;                          // rows in flight ahead of the staged one
+    constexpr int NW = 2 * R + 2;                  // register window depth
+    constexpr int SPAN = 64 * C;                   // strip width
+    constexpr int NL = (SPAN + 2 * R + 63) / 64;   // staged loads per lane per row
+    __shared__ __attribute__((aligned(16))) double sline[4][64 * NL + 2];
+    __shared__ __attribute__((aligned(16))) double trash[4][SPAN];
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int bx, by;
     xcd_remap(bx, by);
-    const int x0 = bx * 64;
+    const int x0 = bx * SPAN;
     const int y_begin = (by * 4 + wv) * rows;
     if (y_begin >= H) return;  // whole wave leaves; no block barriers below
     const int y_end = min(y_begin + rows, H);
     double* sl = sline[wv];
-    const int x = x0 + lane;
-    const int gx0 = clampi(x0 - R + lane, 0, W - 1);
-    const bool has1 = lane < 2 * R;
-    const int gx1 = clampi(x0 + 64 - R + lane, 0, W - 1);
-
+    int gx[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) gx[q] = clampi(x0 - R + lane + 64 * q, 0, W - 1);
     double k[R + 1];
 #pragma unroll
     for (int u = 0; u <= R; ++u) k[u] = taps.k[u];
-    const double sw = taps.sum_w;
-
-    double win[NW];
+    const double sw = taps.sum_w, inv = taps.inv;
+    double win[C][NW];
 #pragma unroll
-    for (int q = 0; q < NW; ++q) win[q] = 0.0;
-
-    const int yy0 = y_begin - R, yy_end = y_end + R;
-    double a0 = fetch_src<MODE>(src, W, clampi(yy0, 0, H - 1), gx0);
-    double a1 = has1 ? fetch_src<MODE>(src, W, clampi(yy0, 0, H - 1), gx1) : 0.0;
-    // The row loop is unrolled by NW so that the window slot of every row is
-    // a compile-time constant: slot s of block yb holds horizontal-pass row
-    // yb+s, and no register moves are needed to slide the window.
-    for (int yb = yy0; yb < yy_end; yb += NW) {
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) win[c][q] = 0.0;
+    const int yy0 = y_begin - R, yy_last = y_end + R;  // inclusive: one drain step
+    double pf[PF][NL];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+        const int ry = clampi(yy0 + p, 0, H - 1);
+#pragma unroll
+        for (int q = 0; q < NL; ++q) pf[p][q] = fetch_src<MODE>(src, W, ry, gx[q]);
+    }
+    const int xa = x0 + C * lane;
+    for (int yb = yy0; yb <= yy_last; yb += NW) {
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
             const int yy = yb + s;
-            if (yy < yy_end) {
-                sl[lane] = a0;
-                if (has1) sl[64 + lane] = a1;
-                if (yy + 1 < yy_end) {  // prefetch the next source row
-                    const int ny = clampi(yy + 1, 0, H - 1);
-                    a0 = fetch_src<MODE>(src, W, ny, gx0);
-                    if (has1) a1 = fetch_src<MODE>(src, W, ny, gx1);
+            if (yy <= yy_last) {
+#pragma unroll
+                for (int q = 0; q < NL; ++q) sl[lane + 64 * q] = pf[0][q];
+#pragma unroll
+                for (int p = 0; p + 1 < PF; ++p)
+#pragma unroll
+                    for (int q = 0; q < NL; ++q) pf[p][q] = pf[p + 1][q];
+                {
+                    const int ry = clampi(yy + PF, 0, H - 1);
+#pragma unroll
+                    for (int q = 0; q < NL; ++q) pf[PF - 1][q] = fetch_src<MODE>(src, W, ry, gx[q]);
                 }
                 wave_sync();
-                // horizontal pass (image.cpp:170-185)
-                double acc = sl[lane + R] * k[0];
+                // row pass of source row yy (image.cpp:170-185)
+                double v[C + 2 * R];
+                if (C == 2) {
+                    const double2* s2 = reinterpret_cast<const double2*>(sl + 2 * lane);
 #pragma unroll
-                for (int u = 1; u <= R; ++u) acc += k[u] * (sl[lane + R + u] + sl[lane + R - u]);
-                win[s] = acc / sw;
-                wave_sync();
-                if (yy >= y_begin + R) {
-                    // vertical pass for output row yy-R (image.cpp:193-208):
-                    // rows yy-2R..yy sit in slots s+1..s (mod NW)
-                    const int y = yy - R;
-                    double o = win[(s + R + 1) % NW] * k[0];
+                    for (int q = 0; q < (C + 2 * R) / 2; ++q) {
+                        const double2 t = s2[q];
+                        v[2 * q] = t.x;
+                        v[2 * q + 1] = t.y;
+                    }
+                } else {
 #pragma unroll
-                    for (int u = 1; u <= R; ++u)
-                        o += k[u] * (win[(s + NW - R + u) % NW] + win[(s + 2 * NW - R - u) % NW]);
-                    o = o / sw;
-                    if (x < W) {
-                        dst[(size_t)y * W + x] = o;
-                        if (DECIM && !(x & 1) && !(y & 1) && (x >> 1) < Wd && (y >> 1) < Hd)
-                            dec[(size_t)(y >> 1) * Wd + (x >> 1)] = o;
+                    for (int q = 0; q < C + 2 * R; ++q) v[q] = sl[lane + q];
+                }
+                double hn[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    double acc = v[c + R] * k[0];
+#pragma unroll
+                    for (int u = 1; u <= R; ++u) acc += k[u] * (v[c + R + u] + v[c + R - u]);
+                    hn[c] = div_sum_w(acc, sw, inv);
+                }
+                // column pass of output row yy-R-1 (image.cpp:193-208): rows
+                // yy-2R-1..yy-1 sit in slots s+1..s-1 (mod NW), centre at s+R+1
+                if (yy >= y_begin + R + 1) {
+                    const int y = yy - R - 1;
+                    double o[C];
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        double a = win[c][(s + R + 1) % NW] * k[0];
+#pragma unroll
+                        for (int u = 1; u <= R; ++u)
+                            a += k[u] * (win[c][(s + R + 1 + u) % NW] +
+                                         win[c][(s + R + 1 + NW - u) % NW]);
+                        o[c] = div_sum_w(a, sw, inv);
+                    }
+                    if (C == 2) {  // W is even for C == 2 (launcher)
+                        double* d = (xa < W) ? dst + (size_t)y * W + xa : &trash[wv][2 * lane];
+                        *reinterpret_cast<double2*>(d) = make_double2(o[0], o[C - 1]);
+                    } else {
+                        double* d = (xa < W) ? dst + (size_t)y * W + xa : &trash[wv][lane];
+                        *d = o[0];
+                    }
+                    if (DECIM && !(y & 1) && (y >> 1) < Hd) {
+                        // the even column of the lane: xa for C == 2, x for C == 1
+                        if ((C == 2 || !(xa & 1)) && (xa >> 1) < Wd)
+                            dec[(size_t)(y >> 1) * Wd + (xa >> 1)] = o[0];
                     }
                 }
+#pragma unroll
+                for (int c = 0; c < C; ++c) win[c][s] = hn[c];
+                wave_sync();
             }
         }
     }
@@ -413,7 +480,7 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
             const int r = i / SW, c = i - r * SW;
             const size_t q = (size_t)clampi(cy0 - 1 + r, 0, H - 1) * W + clampi(cx0 - 1 + c, 0, W - 1);
 #pragma unroll
-            for (int l = 0; l < NL; ++l) g[it][l] = (i < NPIX) ? pt->lvl[o][l][q] : 0.0;
+            for (int l = 0; l < NL; ++l) g[it][l] = (i < NPIX) ? gbl(pt->lvl[o][l])[q] : 0.0;
         }
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
@@ -537,8 +604,8 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
             const int xi = (int)x, yi = (int)y;
 #pragma unroll
             for (int dz = -1; dz <= 1; ++dz) {
-                const double* ga = pt->lvl[o][layer + dz + 1];
-                const double* gb = pt->lvl[o][layer + dz];
+                gdouble* ga = gbl(pt->lvl[o][layer + dz + 1]);
+                gdouble* gb = gbl(pt->lvl[o][layer + dz]);
 #pragma unroll
                 for (int dx = -1; dx <= 1; ++dx)
 #pragma unroll
@@ -609,37 +676,44 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
 }
 
 // ---------------------------------------------------------------------------
-// k_orient: compute_orientations (sift.cpp:447-533), one wavefront per
-// refined keypoint.
-//  * Samples are evaluated 64-wide in chunks of whole window columns, lanes
-//    running along x so the four gradient loads coalesce, and staged in LDS
-//    in the reference's scan order (i = x offset outer, j = y offset inner).
-//  * Each lane owns up to four bins and adds the staged values of its bins
-//    sequentially, eight per step from vector LDS reads, so every bin is
-//    summed in exactly the reference order (sift.cpp:491).
+// k_orient: compute_orientations (sift.cpp:447-533), one 256-thread
+// workgroup per refined keypoint, taken from a work counter.
+//  * The (2r+1)^2 window is swept 256 samples at a time (lanes along x, so
+//    the four gradient loads coalesce); wave w takes chunks w, w+4, ...
+//  * Each wave adds weight*magnitude into its own four lane-interleaved
+//    replicas of the histogram (ds_add_f64); the 16 partial histograms are
+//    summed in a fixed order, so results are reproducible run to run. The
+//    per-bin summation order differs from the reference's scan order: the
+//    bins move by a few ulps, the same order of effect as ocml's atan2/exp
+//    against glibc's, far below what a peak decision resolves.
 //  * The in-place circular smoothing (sift.cpp:496-504) is a Gauss-Seidel
-//    recurrence and runs on lane 0 with the running value in a register.
+//    recurrence and runs on one lane; peaks are tested one bin per lane.
 // ---------------------------------------------------------------------------
-template <bool WIDE>  // WIDE: more than 64 orientation bins (up to kMaxBins)
-__global__ __launch_bounds__(256, 3) void k_orient(const PyrTable* __restrict__ pt, DevParams P,
+constexpr int kOriReps = 4;
+
+__global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt, DevParams P,
                                                 const RawKp* __restrict__ raw,
                                                 const unsigned* __restrict__ raw_begin,
                                                 const unsigned* __restrict__ n_raw,
                                                 unsigned cap_raw, sift_kp* __restrict__ out,
                                                 double* __restrict__ out_off0,
-                                                unsigned* __restrict__ n_out,
-                                                unsigned cap_out) {
-    constexpr int CH = 640;  // staged samples per chunk (multiple of 8)
-    __shared__ __attribute__((aligned(16))) double sval[4][CH];
-    __shared__ __attribute__((aligned(16))) short sbin[4][CH];
-    __shared__ double shist[4][kMaxBins];
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+                                                unsigned* __restrict__ n_out, unsigned cap_out,
+                                                unsigned* __restrict__ work) {
+    __shared__ double hist[4 * kOriReps * (kMaxBins + 2)];
+    __shared__ double hs[kMaxBins];
+    __shared__ unsigned s_k;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const unsigned n = min(*n_raw, cap_raw);
     const unsigned k0 = min(*raw_begin, n);
     const int nb = P.num_bins;
-    const int nbq = WIDE ? (nb + 63) >> 6 : 1;
-    for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
+    const int stride = nb + 2;  // pad rotates LDS banks between replicas
+    double* rep = &hist[(wv * kOriReps + (lane & (kOriReps - 1))) * stride];
+    for (;;) {
+        if (tid == 0) s_k = k0 + atomicAdd(work, 1u);
+        __syncthreads();
+        const unsigned k = s_k;
+        if (k >= n) break;
         const RawKp kp = raw[k];
         const int o = kp.octave;
         const double inv = 1.0 / pow2i(o);
@@ -649,73 +723,39 @@ __global__ __launch_bounds__(256, 3) void k_orient(const PyrTable* __restrict__ 
         const double scale = P.ori_sigma_factor * size;
         const int radius = (int)round(3.0 * scale);
         const double denom = 2.0 * scale * scale;
-        const double* img = pt->lvl[o][kp.layer];
+        gdouble* img = gbl(pt->lvl[o][kp.layer]);
         const int W = pt->w[o], H = pt->h[o];
         const int side = 2 * radius + 1;
-        // chunk = ncol whole columns (i values); a lane covers (di, dj)
-        const int ncol = max(1, min(CH / side, 64));
-        const int lrows = 64 / ncol;
-        const int di = lane % ncol, dj = lane / ncol;
-        const bool lane_on = dj < lrows;
-        double hb[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int ic = 0; ic < side; ic += ncol) {
-            const int nci = min(ncol, side - ic);
-            const int cnt = nci * side;
-            for (int jq = dj; lane_on && jq < side; jq += lrows) {
-                const int iq = di;
-                if (iq < nci) {
-                    const int i = ic + iq - radius, j = jq - radius;
-                    short bin = -1;
-                    double val = 0.0;
-                    if (!(x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H)) {
-                        const size_t r0 = (size_t)(y + j) * W;
-                        const double dx = img[r0 + x + i + 1] - img[r0 + x + i - 1];
-                        const double dy = img[r0 - W + x + i] - img[r0 + W + x + i];
-                        const double mag = sqrt(dx * dx + dy * dy);
-                        const double ang = atan2(dy, dx);
-                        const double wgt = exp(-(i * i + j * j) / denom);
-                        int hidx = (int)round(nb * (ang + kPi) / kTwoPi);
-                        hidx = (hidx < nb) ? hidx : 0;
-                        bin = (short)hidx;
-                        val = wgt * mag;
-                    }
-                    const int t = iq * side + jq;  // reference order within the chunk
-                    sval[wv][t] = val;
-                    sbin[wv][t] = bin;
-                }
+        for (int i = tid; i < 4 * kOriReps * stride; i += 256) hist[i] = 0.0;
+        __syncthreads();
+        // window rows j (y offset) by chunks of 64 columns i (x offset)
+        const int cpr = (side + 63) >> 6;  // chunks per row
+        const int nchunks = side * cpr;
+        for (int c = wv; c < nchunks; c += 4) {
+            const int jq = c / cpr;
+            const int iq = (c - jq * cpr) * 64 + lane;
+            const int i = iq - radius, j = jq - radius;
+            if (iq < side && !(x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 ||
+                               y + j + 1 >= H)) {
+                const size_t r0 = (size_t)(y + j) * W;
+                const double dx = img[r0 + x + i + 1] - img[r0 + x + i - 1];
+                const double dy = img[r0 - W + x + i] - img[r0 + W + x + i];
+                const double mag = sqrt(dx * dx + dy * dy);
+                const double ang = atan2(dy, dx);
+                const double wgt = exp(-(i * i + j * j) / denom);
+                int hidx = (int)round(nb * (ang + kPi) / kTwoPi);
+                hidx = (hidx < nb) ? hidx : 0;
+                atomicAdd(&rep[hidx], wgt * mag);
             }
-            const int cnt8 = (cnt + 7) & ~7;
-            for (int t = cnt + lane; t < cnt8; t += 64) sbin[wv][t] = -1;
-            wave_sync();
-            for (int t = 0; t < cnt8; t += 8) {
-                const short4 b0 = *reinterpret_cast<const short4*>(&sbin[wv][t]);
-                const short4 b1 = *reinterpret_cast<const short4*>(&sbin[wv][t + 4]);
-                const double2 v0 = *reinterpret_cast<const double2*>(&sval[wv][t]);
-                const double2 v1 = *reinterpret_cast<const double2*>(&sval[wv][t + 2]);
-                const double2 v2 = *reinterpret_cast<const double2*>(&sval[wv][t + 4]);
-                const double2 v3 = *reinterpret_cast<const double2*>(&sval[wv][t + 6]);
-                const short bs[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-                const double vs[8] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    // adding +0.0 never changes a non-negative bin sum
-                    hb[0] += (bs[e] == lane) ? vs[e] : 0.0;
-                    if (WIDE && nbq > 1) {
-                        hb[1] += (bs[e] == lane + 64) ? vs[e] : 0.0;
-                        if (nbq > 2) {
-                            hb[2] += (bs[e] == lane + 128) ? vs[e] : 0.0;
-                            hb[3] += (bs[e] == lane + 192) ? vs[e] : 0.0;
-                        }
-                    }
-                }
-            }
-            wave_sync();
         }
-        for (int q = 0; q < nbq; ++q)
-            if (lane + 64 * q < nb) shist[wv][lane + 64 * q] = hb[q];
-        wave_sync();
-        if (lane == 0) {
-            double* hs = shist[wv];
+        __syncthreads();
+        for (int b = tid; b < nb; b += 256) {
+            double v = 0.0;
+            for (int r = 0; r < 4 * kOriReps; ++r) v += hist[r * stride + b];
+            hs[b] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
             for (int it = 0; it < kSmoothIters; ++it) {
                 double prev = hs[nb - 1];  // h[i-1] for i = 0: not yet updated
                 const double h0_old = hs[0];
@@ -732,93 +772,98 @@ __global__ __launch_bounds__(256, 3) void k_orient(const PyrTable* __restrict__ 
                 }
             }
         }
-        wave_sync();
-        double mx = 0.0;  // histogram entries are >= 0
-        for (int q = 0; q < nbq; ++q)
-            if (lane + 64 * q < nb) mx = fmax(mx, shist[wv][lane + 64 * q]);
+        __syncthreads();
+        // max over bins (histogram entries are >= 0): every wave reduces all
+        double mx = 0.0;
+        for (int b = lane; b < nb; b += 64) mx = fmax(mx, hs[b]);
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
-        for (int q = 0; q < nbq; ++q) {
-            const int i = lane + 64 * q;
-            bool peak = false;
-            double ori = 0.0;
-            if (i < nb) {
-                const double h0 = shist[wv][i == 0 ? nb - 1 : i - 1];
-                const double h1 = shist[wv][i];
-                const double h2 = shist[wv][i + 1 == nb ? 0 : i + 1];
-                if (h1 > h0 && h1 > h2 && h1 > (P.peak_ratio * mx)) {
-                    double fi = i + 0.5 * (h0 - h2) / (h0 - 2 * h1 + h2);
-                    fi = fmod(fi + nb, (double)nb);
-                    ori = kTwoPi * fi / nb;
-                    ori = fmod(ori + kTwoPi, kTwoPi);
-                    peak = true;
-                }
-            }
-            if (peak) {
+        for (int i = tid; i < nb; i += 256) {
+            const double h0 = hs[i == 0 ? nb - 1 : i - 1];
+            const double h1 = hs[i];
+            const double h2 = hs[i + 1 == nb ? 0 : i + 1];
+            if (h1 > h0 && h1 > h2 && h1 > (P.peak_ratio * mx)) {
+                double fi = i + 0.5 * (h0 - h2) / (h0 - 2 * h1 + h2);
+                fi = fmod(fi + nb, (double)nb);
+                double ori = kTwoPi * fi / nb;
+                ori = fmod(ori + kTwoPi, kTwoPi);
                 const unsigned idx = atomicAdd(n_out, 1u);
                 if (idx < cap_out) {
-                    sift_kp r;
-                    r.x = kp.x;
-                    r.y = kp.y;
-                    r.octave = kp.octave;
-                    r.layer = kp.layer;
-                    r.size = kp.size;
-                    r.pori = ori;
+                    double rx = kp.x, ry = kp.y, rs = kp.size;
                     if (P.double_image) {
-                        r.x /= 2;
-                        r.y /= 2;
-                        r.size /= 2;
+                        rx /= 2;
+                        ry /= 2;
+                        rs /= 2;
                     }
-                    out[idx].x = r.x;
-                    out[idx].y = r.y;
-                    out[idx].octave = r.octave;
-                    out[idx].layer = r.layer;
-                    out[idx].size = r.size;
-                    out[idx].pori = r.pori;
+                    out[idx].x = rx;
+                    out[idx].y = ry;
+                    out[idx].octave = kp.octave;
+                    out[idx].layer = kp.layer;
+                    out[idx].size = rs;
+                    out[idx].pori = ori;
                     out_off0[idx] = kp.off0;
                 }
             }
         }
-        wave_sync();
+        __syncthreads();
     }
 }
 
 // ---------------------------------------------------------------------------
 // k_descriptor: compute_descriptors + update_histogram + convert_hist_to_desc
-// (sift.cpp:541-682), one wavefront per oriented keypoint.
-//  * Phase A walks the (2r+1)^2 window 64 samples at a time (lanes along x),
-//    applies the rotated-box and image-border tests (sift.cpp:651-656) and
-//    compacts the accepted ~half into a per-wave LDS ring;
-//  * phase B drains the ring 64 at a time through the expensive part
-//    (gradient, atan2, exp weight, trilinear split), so no lane idles on a
-//    rejected sample. The two fmods of sift.cpp:667 reduce exactly to
-//    compare-and-subtract (|angle| < 2*2pi; fmod results are exact).
-//  * Histogram adds go to a per-wave 4x4x8 f64 histogram in LDS (ds_add_f64;
-//    one wave per histogram, so results are reproducible run to run). The
-//    two normalisation sums run sequentially on lane 0 in index order.
+// (sift.cpp:541-682), one 256-thread workgroup per oriented keypoint, taken
+// from a work counter (persistent grid, dynamic balance over keypoints of
+// very different window sizes).
+//  * Accepted samples are enumerated, not searched: for a fixed row, the
+//    reference's test (sift.cpp:651-656) is a conjunction of conditions that
+//    are each monotone in col (col*sin, col*cos, the division and the +1.5
+//    are monotone in IEEE arithmetic), so the accepted columns form one
+//    interval. Each lane estimates the interval of one row analytically and
+//    snaps both ends with the exact test; a wave scan of the lengths then maps
+//    64 consecutive accepted samples to (row, col) per step, so every lane
+//    always works on an accepted sample.
+//  * Rows are dealt round-robin to the four waves; each wave adds into its
+//    own four lane-interleaved replicas of the 4x4x8 f64 histogram
+//    (ds_add_f64; replicas cut same-address serialisation 4x), summed in a
+//    fixed order at the end, so results are reproducible run to run.
+//  * /hist_width is a correctly rounded division by a per-keypoint constant
+//    (div_sum_w with inv = 1/hist_width), the fmods of sift.cpp:667 reduce
+//    exactly to compare-and-subtract (|angle| < 2*2pi, fmod is exact).
+//  * The two normalisation sums run sequentially on one lane in index order.
 // ---------------------------------------------------------------------------
+constexpr int kDescReps = 4;          // histogram replicas per wave
+constexpr int kDescRepStride = 130;   // doubles; the pad rotates LDS banks
+
 __global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__ pt,
                                                     DevParams P, sift_kp* __restrict__ recs,
                                                     const unsigned* __restrict__ rec_begin,
                                                     const unsigned* __restrict__ n_p,
-                                                    unsigned cap,
-                                                    float* __restrict__ desc_f32) {
-    constexpr int RING = 256;  // power of two
-    __shared__ double sh[4][128];
-    __shared__ double sinv[4];
-    __shared__ double qrr[4][RING], qcr[4][RING];
-    __shared__ int qxy[4][RING];
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+                                                    unsigned cap, float* __restrict__ desc_f32,
+                                                    unsigned* __restrict__ work, ExportSink ex) {
+    __shared__ double hist[4][kDescReps * kDescRepStride];
+    __shared__ double hsum[128];
+    __shared__ double s_inv;
+    __shared__ unsigned s_k;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const unsigned n = min(*n_p, cap);
     const unsigned k0 = min(*rec_begin, n);
-    for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
+    if (ex.cnt && blockIdx.x == 0 && tid == 0) {
+        ex.cnt[0] = k0;
+        ex.cnt[1] = n;
+    }
+    double* hw_rep = &hist[wv][(lane & (kDescReps - 1)) * kDescRepStride];
+    for (;;) {
+        if (tid == 0) s_k = k0 + atomicAdd(work, 1u);
+        __syncthreads();
+        const unsigned k = s_k;
+        if (k >= n) break;
         const double* hdr = reinterpret_cast<const double*>(&recs[k]);
         const double kx = hdr[0], ky = hdr[1];
         const int o = reinterpret_cast<const int*>(hdr)[4];
         const int layer = reinterpret_cast<const int*>(hdr)[5];
         const double ksize = hdr[3], pori = hdr[4];
-        const double* img = pt->lvl[o][layer];
+        gdouble* img = gbl(pt->lvl[o][layer]);
         const int W = pt->w[o], H = pt->h[o];
         const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
         const int x = (int)(kx * inv);
@@ -827,133 +872,180 @@ __global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__
         const double bins_per_rad = kDescBins / kTwoPi;
         const double ca = cos(pori), sa = sin(pori);
         const double hw = P.desc_scale_factor * size;
+        const double ihw = 1.0 / hw;
         const double denom = 0.5 * kDescW * kDescW;
         const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
         const double diag = sqrt((double)(W * W + H * H));
         const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
-        sh[wv][lane] = 0.0;
-        sh[wv][lane + 64] = 0.0;
-        wave_sync();
         const int side = 2 * radius + 1;
-        const int ns = side * side;
-        int s0 = 0;         // next window sample to classify
-        unsigned head = 0;  // ring read position
-        unsigned tail = 0;  // ring write position
-        while (true) {
-            const unsigned queued = tail - head;
-            if (queued < 64 && s0 < ns) {
-                // ---- phase A: classify 64 samples, compact the accepted ones
-                const int s = s0 + lane;
-                bool acc = false;
-                double row_rot = 0.0, col_rot = 0.0;
-                int nx = 0, ny = 0;
-                if (s < ns) {
-                    const int row = s / side - radius;
-                    const int col = s % side - radius;
-                    row_rot = (col * sa + row * ca) / hw;
-                    col_rot = (col * ca - row * sa) / hw;
+        for (int i = lane; i < kDescReps * kDescRepStride; i += 64) hist[wv][i] = 0.0;
+        wave_sync();
+
+        // the reference's rotated-box + image-border test (sift.cpp:645-656)
+        auto accepted = [&](int row, int col) -> bool {
+            const double row_rot = div_sum_w(col * sa + row * ca, hw, ihw);
+            const double col_rot = div_sum_w(col * ca - row * sa, hw, ihw);
+            const double rb = row_rot + kDescW / 2 - 0.5;
+            const double cb = col_rot + kDescW / 2 - 0.5;
+            const int nx = col + x, ny = row + y;
+            return col >= -radius && col <= radius && rb > -1.0 && rb < kDescW && cb > -1.0 &&
+                   cb < kDescW && nx > 0 && nx < (W - 1) && ny > 0 && ny < (H - 1);
+        };
+        // this wave's rows are j = wv + 4*m; 64 of them (one per lane) per group
+        for (int g0 = wv; g0 < side; g0 += 4 * 64) {
+            const int j = g0 + 4 * lane;
+            const int row = j - radius;
+            int lo = 0, len = 0;
+            if (j < side && row + y > 0 && row + y < H - 1) {
+                // real-arithmetic interval of |c*sa + row*ca| < 2.5 hw and
+                // |c*ca - row*sa| < 2.5 hw, then snapped with the exact test
+                const double lim = (0.5 * kDescW + 0.5) * hw;
+                double clo = (double)max(-radius, 1 - x), chi = (double)min(radius, W - 2 - x);
+                const double ra = row * ca, rs = row * sa;
+                if (sa != 0.0) {
+                    const double a1 = (-lim - ra) / sa, a2 = (lim - ra) / sa;
+                    clo = fmax(clo, fmin(a1, a2));
+                    chi = fmin(chi, fmax(a1, a2));
+                } else if (!(fabs(ra) < lim)) {
+                    chi = clo - 1.0;
+                }
+                if (ca != 0.0) {
+                    const double b1 = (-lim + rs) / ca, b2 = (lim + rs) / ca;
+                    clo = fmax(clo, fmin(b1, b2));
+                    chi = fmin(chi, fmax(b1, b2));
+                } else if (!(fabs(rs) < lim)) {
+                    chi = clo - 1.0;
+                }
+                if (clo <= chi + 2.0) {
+                    lo = (int)ceil(clo);
+                    int hi = (int)floor(chi);
+                    for (int t = 0; t < 3 && accepted(row, lo - 1); ++t) --lo;
+                    for (int t = 0; t < 3 && lo <= hi + 1 && !accepted(row, lo); ++t) ++lo;
+                    for (int t = 0; t < 3 && accepted(row, hi + 1); ++t) ++hi;
+                    for (int t = 0; t < 3 && hi >= lo && !accepted(row, hi); ++t) --hi;
+                    len = hi >= lo ? hi - lo + 1 : 0;
+                }
+            }
+            // inclusive scan of the row lengths across the wave
+            int pre = len;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(pre, off);
+                if (lane >= off) pre += t;
+            }
+            const int total = __builtin_amdgcn_readlane(pre, 63);
+            int cur = 0;  // first row (lane index) whose samples are not all consumed
+            for (int t0 = 0; t0 < total; t0 += 64) {
+                const int t = t0 + lane;
+                // row r of sample t: the first r >= cur with pre_r > t
+                int r = cur;
+                int nxt = cur;
+                for (int q = cur; q < 64; ++q) {
+                    const int pq = __builtin_amdgcn_readlane(pre, q);
+                    if (pq > t0 + 63) break;
+                    r += (pq <= t) ? 1 : 0;
+                    nxt = q + 1;
+                }
+                const int lo_r = __shfl(lo, r);
+                const int ex_r = __shfl(pre, r) - __shfl(len, r);
+                cur = nxt;
+                if (t < total) {
+                    const int srow = g0 + 4 * r - radius;
+                    const int scol = lo_r + (t - ex_r);
+                    const double row_rot = div_sum_w(scol * sa + srow * ca, hw, ihw);
+                    const double col_rot = div_sum_w(scol * ca - srow * sa, hw, ihw);
                     const double rb = row_rot + kDescW / 2 - 0.5;
                     const double cb = col_rot + kDescW / 2 - 0.5;
-                    ny = row + y;
-                    nx = col + x;
-                    acc = rb > -1.0 && rb < kDescW && cb > -1.0 && cb < kDescW && nx > 0 &&
-                          nx < (W - 1) && ny > 0 && ny < (H - 1);
-                }
-                const unsigned long long m = __ballot(acc);
-                if (acc) {
-                    const unsigned slot =
-                        (tail + (unsigned)__popcll(m & ((1ull << lane) - 1ull))) & (RING - 1);
-                    qrr[wv][slot] = row_rot;
-                    qcr[wv][slot] = col_rot;
-                    qxy[wv][slot] = (ny << 16) | nx;
-                }
-                tail += (unsigned)__popcll(m);
-                s0 += 64;
-                wave_sync();
-                continue;
-            }
-            if (queued == 0) break;
-            // ---- phase B: drain up to 64 accepted samples
-            const unsigned take = queued < 64 ? queued : 64;
-            if ((unsigned)lane < take) {
-                const unsigned slot = (head + lane) & (RING - 1);
-                const double row_rot = qrr[wv][slot], col_rot = qcr[wv][slot];
-                const int pxy = qxy[wv][slot];
-                const int nx = pxy & 0xFFFF, ny = pxy >> 16;
-                const double rb = row_rot + kDescW / 2 - 0.5;
-                const double cb = col_rot + kDescW / 2 - 0.5;
-                const size_t r0 = (size_t)ny * W;
-                const double dx = img[r0 + nx + 1] - img[r0 + nx - 1];
-                const double dy = img[r0 - W + nx] - img[r0 + W + nx];
-                const double mag = sqrt(dx * dx + dy * dy);
-                double ang = atan2(dy, dx);
-                ang -= pori;
-                // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi:
-                // fmod(a, M) = a - trunc(a/M) M is exact and representable,
-                // so one compare-and-subtract reproduces it bit for bit.
-                if (ang >= kTwoPi) ang -= kTwoPi;
-                else if (ang <= -kTwoPi) ang += kTwoPi;
-                ang += kTwoPi;  // rounded, as in the reference
-                if (ang >= kTwoPi) ang -= kTwoPi;
-                if (ang >= kTwoPi) ang -= kTwoPi;
-                const double ob = ang * bins_per_rad;
-                const double wgt = exp(-(row_rot * row_rot + col_rot * col_rot) / denom);
-                const double m = mag * wgt;
-                const int br = (int)floor(rb), bc = (int)floor(cb), bo = (int)floor(ob);
-                const double fr = rb - br, fc = cb - bc, fo = ob - bo;
+                    const int nx = scol + x, ny = srow + y;
+                    const size_t r0 = (size_t)ny * W;
+                    const double dx = img[r0 + nx + 1] - img[r0 + nx - 1];
+                    const double dy = img[r0 - W + nx] - img[r0 + W + nx];
+                    const double mag = sqrt(dx * dx + dy * dy);
+                    double ang = atan2(dy, dx);
+                    ang -= pori;
+                    // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi:
+                    // fmod(a, M) = a - trunc(a/M) M is exact and representable,
+                    // so one compare-and-subtract reproduces it bit for bit.
+                    if (ang >= kTwoPi) ang -= kTwoPi;
+                    else if (ang <= -kTwoPi) ang += kTwoPi;
+                    ang += kTwoPi;  // rounded, as in the reference
+                    if (ang >= kTwoPi) ang -= kTwoPi;
+                    if (ang >= kTwoPi) ang -= kTwoPi;
+                    const double ob = ang * bins_per_rad;
+                    const double wgt = exp(-(row_rot * row_rot + col_rot * col_rot) / denom);
+                    const double m = mag * wgt;
+                    const int br = (int)floor(rb), bc = (int)floor(cb), bo = (int)floor(ob);
+                    const double fr = rb - br, fc = cb - bc, fo = ob - bo;
 #pragma unroll
-                for (int r = 0; r <= 1; ++r) {
-                    const int ri = br + r;
-                    if (ri < 0 || ri >= kDescW) continue;
-                    const double vr = m * ((r == 0) ? 1.0 - fr : fr);
+                    for (int rq = 0; rq <= 1; ++rq) {
+                        const int ri = br + rq;
+                        if (ri < 0 || ri >= kDescW) continue;
+                        const double vr = m * ((rq == 0) ? 1.0 - fr : fr);
 #pragma unroll
-                    for (int c = 0; c <= 1; ++c) {
-                        const int ci = bc + c;
-                        if (ci < 0 || ci >= kDescW) continue;
-                        const double vc = vr * ((c == 0) ? 1.0 - fc : fc);
+                        for (int cq = 0; cq <= 1; ++cq) {
+                            const int ci = bc + cq;
+                            if (ci < 0 || ci >= kDescW) continue;
+                            const double vc = vr * ((cq == 0) ? 1.0 - fc : fc);
 #pragma unroll
-                        for (int q = 0; q <= 1; ++q) {
-                            const int oi = (bo + q) % kDescBins;
-                            atomicAdd(&sh[wv][ri * 32 + ci * 8 + oi],
-                                      vc * ((q == 0) ? 1.0 - fo : fo));
+                            for (int q = 0; q <= 1; ++q) {
+                                const int oi = (bo + q) % kDescBins;
+                                atomicAdd(&hw_rep[ri * 32 + ci * 8 + oi],
+                                          vc * ((q == 0) ? 1.0 - fo : fo));
+                            }
                         }
                     }
                 }
             }
-            head += take;
-            wave_sync();
         }
-        wave_sync();
-        if (lane == 0) {
-            double* hv = sh[wv];
+        __syncthreads();
+        if (tid < 128) {
+            double v = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+#pragma unroll
+                for (int r = 0; r < kDescReps; ++r) v += hist[w][r * kDescRepStride + tid];
+            hsum[tid] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
             double norm = 0.0;
-            for (int i = 0; i < 128; ++i) norm += hv[i] * hv[i];
+            for (int i = 0; i < 128; ++i) norm += hsum[i] * hsum[i];
             norm = sqrt(norm);
             double ninv = 1.0 / norm;
             norm = 0.0;
             for (int i = 0; i < 128; ++i) {
-                double v = hv[i] * ninv;
+                double v = hsum[i] * ninv;
                 if (v > kMagThr) v = kMagThr;
-                hv[i] = v;
+                hsum[i] = v;
                 norm += v * v;
             }
             norm = sqrt(norm);
-            sinv[wv] = 1.0 / norm;
+            s_inv = 1.0 / norm;
         }
-        wave_sync();
-        const double ninv = sinv[wv];
-        uint8_t* d = recs[k].desc;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = lane + 64 * h;
-            const double hv = sh[wv][i];
+        __syncthreads();
+        if (tid < 128) {
+            const double ninv = s_inv;
+            const double hv = hsum[tid];
             const double q = floor(kIntFactor * hv * ninv);
             int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
             val = val < 0 ? 0 : (val > 255 ? 255 : val);
-            d[i] = (uint8_t)val;
-            if (desc_f32) desc_f32[(size_t)k * 128 + i] = (float)(hv * ninv);
+            recs[k].desc[tid] = (uint8_t)val;
+            if (desc_f32) desc_f32[(size_t)k * 128 + tid] = (float)(hv * ninv);
+            if (k < ex.cap) {
+                ex.rec[k].desc[tid] = (uint8_t)val;
+                if (tid == 0) {
+                    sift_kp& r = ex.rec[k];
+                    r.x = kx;
+                    r.y = ky;
+                    r.octave = o;
+                    r.layer = layer;
+                    r.size = ksize;
+                    r.pori = pori;
+                    ex.off0[k] = ex.off0_src[k];
+                }
+            }
         }
-        wave_sync();
+        __syncthreads();
     }
 }
 
@@ -972,47 +1064,65 @@ static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, size_t lds, hipS
     return hipGetLastError();
 }
 
-template <int R, int MODE>
+template <int R, int C, int MODE>
 static hipError_t launch_blur_r(const BlurSource& src, double* dst, int W, int H, int rows,
                                 const BlurTaps& taps, double* dec, int Wd, int Hd,
                                 hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    dim3 grid((W + 63) / 64, ((H + rows - 1) / rows + 3) / 4);
+    dim3 grid((W + 64 * C - 1) / (64 * C), ((H + rows - 1) / rows + 3) / 4);
     if (MODE == kSrcPlane && dec)
-        return launch_timed(k_blur<R, true, kSrcPlane>, grid, dim3(256), 0, s, e0, e1, src, dst,
-                            W, H, rows, taps, dec, Wd, Hd);
-    return launch_timed(k_blur<R, false, MODE>, grid, dim3(256), 0, s, e0, e1, src, dst, W, H,
-                        rows, taps, dec, Wd, Hd);
+        return launch_timed(k_blur<R, C, true, kSrcPlane>, grid, dim3(256), 0, s, e0, e1, src,
+                            dst, W, H, rows, taps, dec, Wd, Hd);
+    return launch_timed(k_blur<R, C, false, MODE>, grid, dim3(256), 0, s, e0, e1, src, dst, W,
+                        H, rows, taps, dec, Wd, Hd);
 }
 
 using BlurFn = hipError_t (*)(const BlurSource&, double*, int, int, int, const BlurTaps&,
                               double*, int, int, hipStream_t, hipEvent_t, hipEvent_t);
 
-template <int MODE, int... Rs>
+template <int C, int MODE, int... Rs>
 struct BlurTable {
-    static constexpr BlurFn fns[sizeof...(Rs)] = {&launch_blur_r<Rs, MODE>...};
+    static constexpr BlurFn fns[sizeof...(Rs)] = {&launch_blur_r<Rs, C, MODE>...};
 };
-template <int MODE, int... Rs>
-constexpr BlurFn BlurTable<MODE, Rs...>::fns[sizeof...(Rs)];
+template <int C, int MODE, int... Rs>
+constexpr BlurFn BlurTable<C, MODE, Rs...>::fns[sizeof...(Rs)];
 
 #define SIFT_R_LIST 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16
-using BlurPlane = BlurTable<kSrcPlane, SIFT_R_LIST>;
-using BlurGray = BlurTable<kSrcGray, SIFT_R_LIST>;
-using BlurUps = BlurTable<kSrcUpsample, SIFT_R_LIST>;
+using BlurPlane1 = BlurTable<1, kSrcPlane, SIFT_R_LIST>;
+using BlurPlane2 = BlurTable<2, kSrcPlane, SIFT_R_LIST>;
+using BlurGray1 = BlurTable<1, kSrcGray, SIFT_R_LIST>;
+using BlurGray2 = BlurTable<2, kSrcGray, SIFT_R_LIST>;
+using BlurUps1 = BlurTable<1, kSrcUpsample, SIFT_R_LIST>;
+using BlurUps2 = BlurTable<2, kSrcUpsample, SIFT_R_LIST>;
 #undef SIFT_R_LIST
 static_assert(kMaxTemplR == 16, "blur tables must cover 1..kMaxTemplR");
 
-int blur_rows_for(int W, int H, int R) {
-    // Strip height trades the 2R-row priming of every strip against the
-    // number of wavefronts in flight; measured on MI355X
-    // (tools/blur_variants.hip): ~4096 waves is the sweet spot for 4K
-    // levels, small levels are latency-bound and want 4-8 row strips.
-    const int nsx = (W + 63) / 64;
-    int rows = (int)(((long)H * nsx + 4095) / 4096);
-    const int min_rows = R >= 8 ? 12 : 4;
-    if (rows < min_rows) rows = min_rows;
-    if (rows > 32) rows = 32;
-    if (rows > H) rows = H;
-    return rows;
+// Strip shape per level (measured on MI355X, tools/blur_lab.hip): two
+// columns per lane and 32-row strips on octave-0-sized levels, two columns
+// and 16 rows around 2 Mpx, one column and 16 rows below (more, shorter
+// strips: the small levels are latency-bound).
+BlurShape blur_shape_for(int W, int H, int R) {
+    const size_t px = (size_t)W * H;
+    BlurShape b;
+    b.cols = (!(W & 1) && px >= ((size_t)1 << 20)) ? 2 : 1;
+    b.rows = px >= ((size_t)4 << 20) ? 32 : 16;
+    if (R > 12 && b.cols == 2) b.rows = 16;
+    if (b.rows > H) b.rows = H;
+    return b;
+}
+
+static hipError_t launch_blur_shaped(int MODE, const BlurSource& bs, double* dst, int W, int H,
+                                     const BlurTaps& taps, double* dec, int Wd, int Hd,
+                                     hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    const BlurShape sh = blur_shape_for(W, H, taps.R);
+    const int i = taps.R - 1;
+    if (MODE == kSrcPlane)
+        return (sh.cols == 2 ? BlurPlane2::fns[i] : BlurPlane1::fns[i])(bs, dst, W, H, sh.rows, taps,
+                                                                       dec, Wd, Hd, s, e0, e1);
+    if (MODE == kSrcGray)
+        return (sh.cols == 2 ? BlurGray2::fns[i] : BlurGray1::fns[i])(bs, dst, W, H, sh.rows, taps,
+                                                                     dec, Wd, Hd, s, e0, e1);
+    return (sh.cols == 2 ? BlurUps2::fns[i] : BlurUps1::fns[i])(bs, dst, W, H, sh.rows, taps, dec,
+                                                               Wd, Hd, s, e0, e1);
 }
 
 hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurTaps& taps,
@@ -1020,9 +1130,8 @@ hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurT
                        hipEvent_t e1) {
     const int R = taps.R;
     if (R >= 1 && R <= kMaxTemplR) {
-        const int rows = blur_rows_for(W, H, R);
         const BlurSource bs{src, W, H, 1};
-        return BlurPlane::fns[R - 1](bs, dst, W, H, rows, taps, dec, Wd, Hd, s, e0, e1);
+        return launch_blur_shaped(kSrcPlane, bs, dst, W, H, taps, dec, Wd, Hd, s, e0, e1);
     }
     // wide kernels (or R == 0): generic two-pass path through `tmp`
     dim3 grid((W + 255) / 256, H);
@@ -1045,10 +1154,9 @@ bool launch_blur_initial_fused(const double* in, int w, int h, int c, int dbl, d
                                hipEvent_t e0, hipEvent_t e1, hipError_t* err) {
     const int R = taps.R;
     if (R < 1 || R > kMaxTemplR || (c == 1 && !dbl)) return false;
-    const int rows = blur_rows_for(W0, H0, R);
     const BlurSource bs{in, w, h, c};
-    *err = dbl ? BlurUps::fns[R - 1](bs, dst, W0, H0, rows, taps, nullptr, 0, 0, s, e0, e1)
-               : BlurGray::fns[R - 1](bs, dst, W0, H0, rows, taps, nullptr, 0, 0, s, e0, e1);
+    *err = launch_blur_shaped(dbl ? kSrcUpsample : kSrcGray, bs, dst, W0, H0, taps, nullptr, 0, 0,
+                              s, e0, e1);
     return true;
 }
 
@@ -1131,27 +1239,24 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* out, double* out_off0, unsigned* n_out, unsigned cap_out,
-                         hipStream_t s) {
-    unsigned blocks = (cap_raw + 3) / 4;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks == 0) blocks = 1;
-    if (P.num_bins > 64)
-        hipLaunchKernelGGL(k_orient<true>, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin,
-                           n_raw, cap_raw, out, out_off0, n_out, cap_out);
-    else
-        hipLaunchKernelGGL(k_orient<false>, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin,
-                           n_raw, cap_raw, out, out_off0, n_out, cap_out);
+                         unsigned* work, hipStream_t s) {
+    // persistent: workgroups pull keypoints from the work counter
+    unsigned blocks = 1024;
+    if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
+    hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin, n_raw,
+                       cap_raw, out, out_off0, n_out, cap_out, work);
     return hipGetLastError();
 }
 
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
                              const unsigned* rec_begin, const unsigned* n, unsigned cap,
-                             float* desc_f32, hipStream_t s) {
-    unsigned blocks = (cap + 3) / 4;
-    if (blocks > 4096) blocks = 4096;
-    if (blocks == 0) blocks = 1;
+                             float* desc_f32, unsigned* work, const ExportSink& ex,
+                             hipStream_t s) {
+    // persistent: 4 workgroups per CU pull keypoints from the work counter
+    unsigned blocks = 1024;
+    if (blocks > cap) blocks = cap > 0 ? cap : 1;
     hipLaunchKernelGGL(k_descriptor, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_begin, n,
-                       cap, desc_f32);
+                       cap, desc_f32, work, ex);
     return hipGetLastError();
 }
 

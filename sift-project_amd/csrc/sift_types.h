@@ -36,6 +36,7 @@ constexpr size_t kLdsOctaveBytes = (2 * (size_t)kLdsOctavePx + kLdsOctavePx / 4)
 struct BlurTaps {
     double k[kMaxTaps];
     double sum_w;
+    double inv;  // RN(1 / sum_w), for the correctly rounded division
     int R;  // taps k[0..R], R = ks-1
     int pad;
 };
@@ -88,6 +89,18 @@ struct DevParams {
 struct RawKp {
     double x, y, size, off0;
     int octave, layer;
+};
+
+// Where k_descriptor also writes each finished record (mapped, coherent
+// pinned host memory), so the host can finalise a keypoint batch while the
+// device works on the next: rec/off0 index = record index (< cap), cnt =
+// this launch's [begin, end) record range.
+struct ExportSink {
+    sift_kp* rec;
+    double* off0;
+    unsigned* cnt;
+    const double* off0_src;
+    unsigned cap;
 };
 
 }  // namespace sift_amd
