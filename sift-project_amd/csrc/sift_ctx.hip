@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <new>
 #include <vector>
 
@@ -338,18 +339,27 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             break;
         }
     const bool tiles = p->window_size / 2 == 1;
-    // Keypoint batches, one per large octave plus one for the LDS-resident
-    // small octaves, all on stream C: extrema of the batch's octaves, a
-    // snapshot of the counters (the batch's candidate end and its record
-    // begins), then refine over [previous end, this end) -> orientation ->
-    // descriptor over the records appended since the snapshot.
+    // Keypoint batches on stream C: each large octave (>= kBatchPx pixels) is
+    // its own batch as soon as its levels exist; the smaller ones, whose
+    // keypoint work is too small to amortise a chain of launches, form one
+    // final batch. A batch: counter snapshot (its candidate / record begins),
+    // extrema (window 3: with the refine fused in), then orientation +
+    // descriptor of the refined keypoints it appended.
+    constexpr size_t kBatchPx = (size_t)1 << 20;
+    int o_merge = g.octaves;  // first octave of the final batch
+    for (int o = 0; o < g.octaves; ++o)
+        if ((size_t)g.W[o] * g.H[o] < kBatchPx) {
+            o_merge = o;
+            break;
+        }
     const unsigned* zeros = ctx->d_ctr + kCtrZeros;
     auto snap = [&](int g) { return ctx->d_ctr + kCtrSnap + 4 * g; };
     auto launch_extrema_range = [&](int o_begin, int o_end) -> int {
         if (tiles) {
             const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
             SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
-                                              ctx->d_ctr + 0, ctx->cap_cand, sC));
+                                              ctx->d_ctr + 0, ctx->cap_cand, dp, ctx->d_raw,
+                                              ctx->d_ctr + 1, ctx->cap_raw, sC));
         } else {
             for (int o = o_begin; o < o_end; ++o)
                 SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
@@ -358,8 +368,6 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         }
         return SIFT_OK;
     };
-    // refine -> orientation -> descriptor over candidates [cand_begin,
-    // cand_end) and the records they append (ranges from counter snapshots)
     // records of every chain also go to the mapped export buffers, sized from
     // the largest record count seen so far (a larger one falls back to one
     // bulk download at the end, and grows them for the next call)
@@ -367,9 +375,15 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         (st = ctx->exp_off0.ensure(ctx->exp_rec.cap)) != SIFT_OK ||
         (st = ctx->exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
         return st;
+    // poison: a range no launch published reads as "not exported"
+    std::fill(ctx->exp_cnt.h, ctx->exp_cnt.h + ctx->exp_cnt.cap, 0xFFFFFFFFu);
     int n_chains = 0;
-    auto run_chain = [&](const unsigned* cand_begin, const unsigned* cand_end,
-                         const unsigned* begin, hipStream_t sx) -> int {
+    // extrema over [o_begin, o_end) then the keypoint chain. `begin` is a
+    // counter snapshot: taken before the extrema when the refine is fused
+    // (window 3: raw/record begins), after them otherwise (this batch's
+    // candidate end, the next batch's cand_begin), before the refine.
+    auto run_chain = [&](int o_begin, int o_end, const unsigned* cand_begin, unsigned* begin,
+                         bool fused) -> int {
         const int ci = n_chains++;
         unsigned* work = ctx->d_ctr + kCtrWork + 2 * ci;
         while ((int)ctx->chain_ev.size() <= ci) {
@@ -378,31 +392,36 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
                 return SIFT_ERR_HIP;
             ctx->chain_ev.push_back(e);
         }
-        const ExportSink ex{ctx->exp_rec.d, ctx->exp_off0.d, ctx->exp_cnt.d + 2 * ci, ctx->d_off0,
+        const ExportSink ex{ctx->exp_rec.d, ctx->exp_off0.d, ctx->exp_cnt.d + 2 * ci,
                             (unsigned)ctx->exp_rec.cap};
-        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin, cand_end,
-                                   ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, sx));
-        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, begin + 1, ctx->d_ctr + 1,
-                                   ctx->cap_raw, ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2,
-                                   ctx->cap_ori, work, sx));
-        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, begin + 2, ctx->d_ctr + 2,
-                                       ctx->cap_ori, out_desc_f32 ? ctx->d_df32 : nullptr,
-                                       work + 1, ex, sx));
-        SIFT_HIP_TRY(hipEventRecord(ctx->chain_ev[ci], sx));
+        if (fused && begin) SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
+        int st2 = launch_extrema_range(o_begin, o_end);
+        if (st2 != SIFT_OK) return st2;
+        if (!fused) {
+            if (begin) SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
+            SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin, ctx->d_ctr + 0,
+                                       ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw,
+                                       sC));
+        }
+        const unsigned* b = begin ? begin : zeros;
+        SIFT_HIP_TRY(launch_orient_describe(ctx->d_pt, dp, ctx->d_raw, b + 1, ctx->d_ctr + 1,
+                                            ctx->cap_raw, ctx->d_ori, ctx->d_off0, b + 2,
+                                            ctx->d_ctr + 2, ctx->cap_ori,
+                                            out_desc_f32 ? ctx->d_df32 : nullptr, work, ex, sC));
+        SIFT_HIP_TRY(hipEventRecord(ctx->chain_ev[ci], sC));
         return SIFT_OK;
     };
     int n_batches = 0;
-    // batch g: octaves [o_begin, o_end), whose last level was enqueued on sp
-    auto batch = [&](int o_begin, int o_end, hipStream_t sp) -> int {
+    // batch g: octaves [o_begin, o_end), whose levels were enqueued on `sps`
+    auto batch = [&](int o_begin, int o_end, std::initializer_list<hipStream_t> sps) -> int {
         const int gb = n_batches++;
-        hipEvent_t pyr_done = sync_event(ctx, ev_i++);
-        if (!pyr_done) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
-        SIFT_HIP_TRY(hipStreamWaitEvent(sC, pyr_done, 0));
-        int st2 = launch_extrema_range(o_begin, o_end);
-        if (st2 != SIFT_OK) return st2;
-        SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, snap(gb), sC));
-        return run_chain(gb == 0 ? zeros : snap(gb - 1), snap(gb), snap(gb), sC);
+        for (hipStream_t sp : sps) {
+            hipEvent_t pyr_done = sync_event(ctx, ev_i++);
+            if (!pyr_done) return SIFT_ERR_HIP;
+            SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
+            SIFT_HIP_TRY(hipStreamWaitEvent(sC, pyr_done, 0));
+        }
+        return run_chain(o_begin, o_end, gb == 0 ? zeros : snap(gb - 1), snap(gb), tiles);
     };
     // The pyramid alternates between two streams, octave o on pyr[o % 2]:
     // octave o+1 only needs the decimated level `intervals` of octave o, so it
@@ -427,7 +446,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             if (st != SIFT_OK) return st;
             if (dec && (st = next_base_event(so)) != SIFT_OK) return st;
         }
-        if ((st = batch(o, o + 1, so)) != SIFT_OK) return st;
+        if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
     }
     if (o_small < g.octaves) {
         hipStream_t so = pyr[o_small & 1];
@@ -441,8 +460,8 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         if (prof_events(ctx, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(ctx->d_pt, o_small, g.octaves - 1, g.n_gauss,
                                         ctx->d_taps, so, e0, e1));
-        if ((st = batch(o_small, g.octaves, so)) != SIFT_OK) return st;
     }
+    if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
     // stream B joins A (the ctx's public stream) before the call returns
     {
         hipEvent_t j = sync_event(ctx, ev_i++);
@@ -481,9 +500,8 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             exported = false;
             SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
             SIFT_HIP_TRY(hipStreamSynchronize(sC));
-            if ((st = launch_extrema_range(0, g.octaves)) != SIFT_OK) return st;
             n_chains = 0;
-            if ((st = run_chain(zeros, ctx->d_ctr + 0, zeros, sC)) != SIFT_OK) return st;
+            if ((st = run_chain(0, g.octaves, zeros, nullptr, tiles)) != SIFT_OK) return st;
             SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
         }

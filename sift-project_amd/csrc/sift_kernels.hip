@@ -291,36 +291,70 @@ struct LdsLevel {
     bool dec;
 };
 
+// One level: every thread takes runs of kLdsRun consecutive outputs (along
+// x in the row pass, along y in the column pass), loads the run plus its 2R
+// halo once from LDS and evaluates the kLdsRun independent dependency chains
+// interleaved (one output per thread was LDS- and latency-bound: 2R+1 reads
+// and one serial chain per output, on one CU).
+constexpr int kLdsRun = 8;
+
 template <int R>
 __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    constexpr int NV = kLdsRun + 2 * R;
     double k[R + 1];
 #pragma unroll
     for (int u = 0; u <= R; ++u) k[u] = t.k[u];
-    const double sw = t.sum_w;
+    const double sw = t.sum_w, inv = t.inv;
     const int W = L.W, H = L.H;
-    for (int y = ty; y < H; y += 16) {
+    // row pass (image.cpp:170-185): task = (row y, run of columns from x0)
+    const int rx = (W + kLdsRun - 1) / kLdsRun;
+    for (int task = threadIdx.x; task < H * rx; task += blockDim.x) {
+        const int y = task / rx;
+        const int x0 = (task - y * rx) * kLdsRun;
         const double* row = L.A + y * W;
-        for (int x = tx; x < W; x += 64) {
-            double acc = row[x] * k[0];
+        double v[NV];
 #pragma unroll
-            for (int u = 1; u <= R; ++u) acc += k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
-            L.T[y * W + x] = acc / sw;
-        }
+        for (int i = 0; i < NV; ++i) v[i] = row[clampi(x0 - R + i, 0, W - 1)];
+        double acc[kLdsRun];
+#pragma unroll
+        for (int j = 0; j < kLdsRun; ++j) acc[j] = v[j + R] * k[0];
+#pragma unroll
+        for (int u = 1; u <= R; ++u)
+#pragma unroll
+            for (int j = 0; j < kLdsRun; ++j) acc[j] += k[u] * (v[j + R + u] + v[j + R - u]);
+#pragma unroll
+        for (int j = 0; j < kLdsRun; ++j)
+            if (x0 + j < W) L.T[y * W + x0 + j] = div_sum_w(acc[j], sw, inv);
     }
     __syncthreads();
-    for (int y = ty; y < H; y += 16) {
-        for (int x = tx; x < W; x += 64) {
-            double acc = L.T[y * W + x] * k[0];
+    // column pass (image.cpp:193-208): task = (column x, run of rows from y0);
+    // consecutive threads take consecutive columns (conflict-free LDS reads)
+    const int ry = (H + kLdsRun - 1) / kLdsRun;
+    for (int task = threadIdx.x; task < W * ry; task += blockDim.x) {
+        const int yr = task / W;
+        const int x = task - yr * W;
+        const int y0 = yr * kLdsRun;
+        double v[NV];
 #pragma unroll
-            for (int u = 1; u <= R; ++u)
-                acc += k[u] * (L.T[min(y + u, H - 1) * W + x] + L.T[max(y - u, 0) * W + x]);
-            const double v = acc / sw;
-            L.A[y * W + x] = v;
-            L.g[y * W + x] = v;
-            if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
-                L.D[(y >> 1) * L.Wd + (x >> 1)] = v;
-                L.gd[(y >> 1) * L.Wd + (x >> 1)] = v;
+        for (int i = 0; i < NV; ++i) v[i] = L.T[clampi(y0 - R + i, 0, H - 1) * W + x];
+        double acc[kLdsRun];
+#pragma unroll
+        for (int j = 0; j < kLdsRun; ++j) acc[j] = v[j + R] * k[0];
+#pragma unroll
+        for (int u = 1; u <= R; ++u)
+#pragma unroll
+            for (int j = 0; j < kLdsRun; ++j) acc[j] += k[u] * (v[j + R + u] + v[j + R - u]);
+#pragma unroll
+        for (int j = 0; j < kLdsRun; ++j) {
+            const int y = y0 + j;
+            if (y < H) {
+                const double o = div_sum_w(acc[j], sw, inv);
+                L.A[y * W + x] = o;
+                L.g[y * W + x] = o;
+                if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
+                    L.D[(y >> 1) * L.Wd + (x >> 1)] = o;
+                    L.gd[(y >> 1) * L.Wd + (x >> 1)] = o;
+                }
             }
         }
     }
@@ -438,6 +472,9 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
         dec[(size_t)(y >> 1) * Wd + (x >> 1)] = o;
 }
 
+__device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, int ex, int ey,
+                           int ez, int o, RawKp* out);
+
 // ---------------------------------------------------------------------------
 // Extrema: detect_octave_extrema + is_extremum (sift.cpp:227-291). A pixel is
 // kept iff |D_z| > threshold (the int threshold of sift.cpp:266,279) and it
@@ -452,13 +489,18 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
 // memory round trip), then each thread takes one column x four centre rows
 // and walks the layers with a rolling window of three layers' 3x3 max/min
 // in registers. Candidates are compacted with a 64-bit ballot per
-// (row, layer) and one atomic per wave.
+// (row, layer) and one atomic per wave. When `raw` is set, every candidate is
+// refined (compute_keypoints, sift.cpp:330-436) by the thread that found it,
+// right after the scan (no separate launch; the tile's pixels are L2-hot).
 template <int NL>
 __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restrict__ pt,
                                                        ExtremaGrid eg, int thr,
                                                        sift_extremum* __restrict__ out,
                                                        unsigned* __restrict__ counter,
-                                                       unsigned cap) {
+                                                       unsigned cap, DevParams P,
+                                                       RawKp* __restrict__ raw,
+                                                       unsigned* __restrict__ n_raw,
+                                                       unsigned cap_raw) {
     constexpr int ND = NL - 1;
     constexpr int TW = 64, TH = 16, SW = TW + 2, SH = TH + 2;
     constexpr int NPIX = SW * SH;             // 1188 staged pixels
@@ -497,6 +539,7 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
     const int r0 = (tid >> 6) * 4;   // first of this thread's four centre rows
     const int x = cx0 + c;
     const double dthr = (double)thr;
+    uint64_t mine = 0;  // this thread's candidates: bit 4*(z-1) + row k
     // rolling 3x3 max/min of layers l-2 (p), l-1 (q), l (n) for 4 centres
     double pmx[4], pmn[4], qmx[4], qmn[4];
 #pragma unroll
@@ -533,6 +576,7 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
                     const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
                     if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, o};
                 }
+                if (cand) mine |= 1ull << (4 * (z - 1) + k);
             }
         }
 #pragma unroll
@@ -541,6 +585,17 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
             pmn[k] = qmn[k];
             qmx[k] = nmx[k];
             qmn[k] = nmn[k];
+        }
+    }
+    if (raw) {
+        while (mine) {
+            const int bit = __builtin_ctzll(mine);
+            mine &= mine - 1;
+            RawKp r;
+            if (refine_one(pt, P, x, cy0 + r0 + (bit & 3), (bit >> 2) + 1, o, &r)) {
+                const unsigned idx = atomicAdd(n_raw, 1u);
+                if (idx < cap_raw) raw[idx] = r;
+            }
         }
     }
 }
@@ -575,11 +630,87 @@ __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// k_refine: compute_keypoints (sift.cpp:330-436) with get_pixel_cube,
-// compute_gradient, compute_hessian, fit_quadratic (sift.cpp:32-106), one
-// thread per candidate, bit-exact (no libm except the size's pow(2, t),
-// which the host recomputes with glibc for the final records).
+// refine_one: compute_keypoints (sift.cpp:330-436) for one candidate, with
+// get_pixel_cube, compute_gradient, compute_hessian, fit_quadratic
+// (sift.cpp:32-106); bit-exact (no libm except the size's pow(2, t), which
+// the host recomputes with glibc for the final records). Called from the
+// extrema kernel right where a candidate is found (window_size 3) and from
+// k_refine (other window sizes).
 // ---------------------------------------------------------------------------
+__device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, int ex, int ey,
+                           int ez, int o, RawKp* out) {
+    const int b = P.window_size / 2;
+    const int W = pt->w[o], H = pt->h[o], depth = P.n_dog;
+    double x = ex, y = ey;
+    int layer = ez;
+    double off0 = 0, off1 = 0, off2 = 0;
+    int step;
+    for (step = 0; step < kMaxSteps; ++step) {
+        double c[3][3][3];
+        const int xi = (int)x, yi = (int)y;
+#pragma unroll
+        for (int dz = -1; dz <= 1; ++dz) {
+            gdouble* ga = gbl(pt->lvl[o][layer + dz + 1]);
+            gdouble* gb = gbl(pt->lvl[o][layer + dz]);
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx)
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy) {
+                    const size_t q = (size_t)(yi + dy) * W + (xi + dx);
+                    c[dz + 1][dx + 1][dy + 1] = (ga[q] - gb[q]) / 255.0;
+                }
+        }
+        const double g0 = 0.5 * (c[2][1][1] - c[0][1][1]);
+        const double g1 = 0.5 * (c[1][2][1] - c[1][0][1]);
+        const double g2 = 0.5 * (c[1][1][2] - c[1][1][0]);
+        const double h00 = c[0][1][1] - 2 * c[1][1][1] + c[2][1][1];
+        const double h11 = c[1][0][1] - 2 * c[1][1][1] + c[1][2][1];
+        const double h22 = c[1][1][0] - 2 * c[1][1][1] + c[1][1][2];
+        const double h01 = 0.25 * (c[2][2][1] - c[2][0][1] - c[0][2][1] + c[0][0][1]);
+        const double h02 = 0.25 * (c[2][1][2] - c[2][1][0] - c[0][1][2] + c[0][1][0]);
+        const double h12 = 0.25 * (c[1][0][0] - c[1][2][0] - c[1][0][2] + c[1][2][2]);
+        const double det = h00 * h11 * h22 + 2 * (h01 * h12 * h02) - h02 * h11 * h02 -
+                           h00 * h12 * h12 - h01 * h01 * h22;
+        const double i00 = (h11 * h22 - h12 * h12) / det;
+        const double i01 = (h02 * h12 - h01 * h22) / det;
+        const double i02 = (h01 * h12 - h02 * h11) / det;
+        const double i11 = (h00 * h22 - h02 * h02) / det;
+        const double i12 = (h02 * h01 - h00 * h12) / det;
+        const double i22 = (h00 * h11 - h01 * h01) / det;
+        off0 = -i00 * g0 - i01 * g1 - i02 * g2;
+        off1 = -i01 * g0 - i11 * g1 - i12 * g2;
+        off2 = -i02 * g0 - i12 * g1 - i22 * g2;
+        const double m = fmax(fabs(off0), fmax(fabs(off1), fabs(off2)));
+        if (m < kConvThr) {
+            const double dot = g0 * off0 + g1 * off1 + g2 * off2;
+            const double val = c[1][1][1] + 0.5 * dot;
+            if (!((fabs(val) * P.intervals) >= P.contrast_threshold)) return false;
+            const double tr = h11 + h22;
+            const double dt = h11 * h22 - h12 * h12;
+            if (tr <= 0) return false;
+            const double er = P.eigen_ratio;
+            if ((tr * tr * er) >= ((er + 1) * (er + 1) * dt)) return false;
+            break;
+        }
+        layer = (int)((double)layer + round(off0));
+        x += round(off1);
+        y += round(off2);
+        if (x < b || x >= (W - b) || y < b || y >= (H - b) || layer < b || layer >= (depth - b))
+            return false;
+    }
+    if (step >= kMaxSteps) return false;
+    const double scale = pow2i(o);
+    out->x = scale * (x + off1);
+    out->y = scale * (y + off2);
+    out->size = P.init_sigma * scale * pow(2.0, ((double)layer + off0) / P.intervals);
+    out->off0 = off0;
+    out->octave = o;
+    out->layer = layer;
+    return true;
+}
+
+// Candidates [cand_begin, n_cand) of the generic-window extrema path, one
+// thread each.
 __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt, DevParams P,
                                                 const sift_extremum* __restrict__ cand,
                                                 const unsigned* __restrict__ cand_begin,
@@ -589,95 +720,27 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
                                                 unsigned cap_out) {
     const unsigned n = min(*n_cand, cap_cand);
     const unsigned i0 = min(*cand_begin, n);
-    const int b = P.window_size / 2;
     for (unsigned i = i0 + blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += gridDim.x * blockDim.x) {
         const sift_extremum e = cand[i];
-        const int o = e.octave;
-        const int W = pt->w[o], H = pt->h[o], depth = P.n_dog;
-        double x = e.x, y = e.y;
-        int layer = e.z;
-        double off0 = 0, off1 = 0, off2 = 0;
-        int step;
-        for (step = 0; step < kMaxSteps; ++step) {
-            double c[3][3][3];
-            const int xi = (int)x, yi = (int)y;
-#pragma unroll
-            for (int dz = -1; dz <= 1; ++dz) {
-                gdouble* ga = gbl(pt->lvl[o][layer + dz + 1]);
-                gdouble* gb = gbl(pt->lvl[o][layer + dz]);
-#pragma unroll
-                for (int dx = -1; dx <= 1; ++dx)
-#pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy) {
-                        const size_t q = (size_t)(yi + dy) * W + (xi + dx);
-                        c[dz + 1][dx + 1][dy + 1] = (ga[q] - gb[q]) / 255.0;
-                    }
-            }
-            const double g0 = 0.5 * (c[2][1][1] - c[0][1][1]);
-            const double g1 = 0.5 * (c[1][2][1] - c[1][0][1]);
-            const double g2 = 0.5 * (c[1][1][2] - c[1][1][0]);
-            const double h00 = c[0][1][1] - 2 * c[1][1][1] + c[2][1][1];
-            const double h11 = c[1][0][1] - 2 * c[1][1][1] + c[1][2][1];
-            const double h22 = c[1][1][0] - 2 * c[1][1][1] + c[1][1][2];
-            const double h01 = 0.25 * (c[2][2][1] - c[2][0][1] - c[0][2][1] + c[0][0][1]);
-            const double h02 = 0.25 * (c[2][1][2] - c[2][1][0] - c[0][1][2] + c[0][1][0]);
-            const double h12 = 0.25 * (c[1][0][0] - c[1][2][0] - c[1][0][2] + c[1][2][2]);
-            const double det = h00 * h11 * h22 + 2 * (h01 * h12 * h02) - h02 * h11 * h02 -
-                               h00 * h12 * h12 - h01 * h01 * h22;
-            const double i00 = (h11 * h22 - h12 * h12) / det;
-            const double i01 = (h02 * h12 - h01 * h22) / det;
-            const double i02 = (h01 * h12 - h02 * h11) / det;
-            const double i11 = (h00 * h22 - h02 * h02) / det;
-            const double i12 = (h02 * h01 - h00 * h12) / det;
-            const double i22 = (h00 * h11 - h01 * h01) / det;
-            off0 = -i00 * g0 - i01 * g1 - i02 * g2;
-            off1 = -i01 * g0 - i11 * g1 - i12 * g2;
-            off2 = -i02 * g0 - i12 * g1 - i22 * g2;
-            const double m = fmax(fabs(off0), fmax(fabs(off1), fabs(off2)));
-            if (m < kConvThr) {
-                const double dot = g0 * off0 + g1 * off1 + g2 * off2;
-                const double val = c[1][1][1] + 0.5 * dot;
-                if (!((fabs(val) * P.intervals) >= P.contrast_threshold)) {
-                    step = kMaxSteps;
-                    break;
-                }
-                const double tr = h11 + h22;
-                const double dt = h11 * h22 - h12 * h12;
-                if (tr <= 0) {
-                    step = kMaxSteps;
-                    break;
-                }
-                const double er = P.eigen_ratio;
-                if ((tr * tr * er) >= ((er + 1) * (er + 1) * dt)) step = kMaxSteps;
-                break;
-            }
-            layer = (int)((double)layer + round(off0));
-            x += round(off1);
-            y += round(off2);
-            if (x < b || x >= (W - b) || y < b || y >= (H - b) || layer < b ||
-                layer >= (depth - b)) {
-                step = kMaxSteps;
-                break;
-            }
-        }
-        if (step >= kMaxSteps) continue;
-        const double scale = pow2i(o);
         RawKp r;
-        r.x = scale * (x + off1);
-        r.y = scale * (y + off2);
-        r.size = P.init_sigma * scale * pow(2.0, ((double)layer + off0) / P.intervals);
-        r.off0 = off0;
-        r.octave = o;
-        r.layer = layer;
+        if (!refine_one(pt, P, e.x, e.y, e.z, e.octave, &r)) continue;
         const unsigned idx = atomicAdd(n_out, 1u);
         if (idx < cap_out) out[idx] = r;
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_orient: compute_orientations (sift.cpp:447-533), one 256-thread
-// workgroup per refined keypoint, taken from a work counter.
+// k_orient_describe: compute_orientations (sift.cpp:447-533) and, for every
+// orientation peak, compute_descriptors + update_histogram +
+// convert_hist_to_desc (sift.cpp:541-682) of the keypoint it makes; one
+// 256-thread workgroup per refined keypoint, taken from a work counter
+// (persistent grid: dynamic balance over windows of very different sizes).
+// Describing every oriented keypoint before clean_keypoints (sift.cpp:762,
+// host) gives the same final records: std::unique only drops records equal
+// in (x, y, size, pori), and the kept one is described from its own fields.
+//
+// Orientation
 //  * The (2r+1)^2 window is swept 256 samples at a time (lanes along x, so
 //    the four gradient loads coalesce); wave w takes chunks w, w+4, ...
 //  * Each wave adds weight*magnitude into its own four lane-interleaved
@@ -688,31 +751,245 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
 //    against glibc's, far below what a peak decision resolves.
 //  * The in-place circular smoothing (sift.cpp:496-504) is a Gauss-Seidel
 //    recurrence and runs on one lane; peaks are tested one bin per lane.
+// Descriptor
+//  * Accepted samples are enumerated, not searched: for a fixed row, the
+//    reference's test (sift.cpp:651-656) is a conjunction of conditions that
+//    are each monotone in col (col*sin, col*cos, the division and the +1.5
+//    are monotone in IEEE arithmetic), so the accepted columns form one
+//    interval. Each lane estimates the interval of one row analytically and
+//    snaps both ends with the exact test; a wave scan of the lengths then maps
+//    64 consecutive accepted samples to (row, col) per step, so every lane
+//    always works on an accepted sample.
+//  * Rows are dealt round-robin to the four waves; each wave adds into its
+//    own four lane-interleaved replicas of the 4x4x8 f64 histogram, summed in
+//    a fixed order at the end.
+//  * /hist_width is a correctly rounded division by a per-keypoint constant
+//    (div_sum_w with inv = 1/hist_width), the fmods of sift.cpp:667 reduce
+//    exactly to compare-and-subtract (|angle| < 2*2pi, fmod is exact).
+//  * The two normalisation sums (sift.cpp:583-596) are fixed-order wave
+//    reductions (the bins themselves are already summed out of the
+//    reference's order, so a sequential sum would buy no exactness).
 // ---------------------------------------------------------------------------
 constexpr int kOriReps = 4;
+constexpr int kDescReps = 4;
+constexpr int kDescRepStride = 130;  // doubles; the pad rotates LDS banks
+constexpr int kKpHist = 4 * kOriReps * (kMaxBins + 2);
+static_assert(kKpHist >= 4 * kDescReps * kDescRepStride, "histogram LDS is shared");
 
-__global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt, DevParams P,
-                                                const RawKp* __restrict__ raw,
-                                                const unsigned* __restrict__ raw_begin,
-                                                const unsigned* __restrict__ n_raw,
-                                                unsigned cap_raw, sift_kp* __restrict__ out,
-                                                double* __restrict__ out_off0,
-                                                unsigned* __restrict__ n_out, unsigned cap_out,
-                                                unsigned* __restrict__ work) {
-    __shared__ double hist[4 * kOriReps * (kMaxBins + 2)];
-    __shared__ double hs[kMaxBins];
-    __shared__ unsigned s_k;
+struct KpLds {
+    double hist[kKpHist];  // replicas: orientation, then descriptor
+    double hs[kMaxBins];   // smoothed orientation histogram
+    double pk[kMaxBins];   // orientations of the peaks
+    double red[4];         // normalisation partial sums
+    unsigned k, npk, rec;
+};
+
+// One descriptor (sift.cpp:610-682) of record `rec`; all 256 threads.
+__device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevParams& P,
+                         sift_kp* __restrict__ recs, unsigned rec, double kx, double ky, int o,
+                         int layer, double ksize, double pori, double off0,
+                         float* __restrict__ desc_f32, const ExportSink& ex) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    double* hw_rep = &S.hist[(wv * kDescReps + (lane & (kDescReps - 1))) * kDescRepStride];
+    gdouble* img = gbl(pt->lvl[o][layer]);
+    const int W = pt->w[o], H = pt->h[o];
+    const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
+    const int x = (int)(kx * inv);
+    const int y = (int)(ky * inv);
+    const double size = ksize * inv;
+    const double bins_per_rad = kDescBins / kTwoPi;
+    const double ca = cos(pori), sa = sin(pori);
+    const double hw = P.desc_scale_factor * size;
+    const double ihw = 1.0 / hw;
+    const double denom = 0.5 * kDescW * kDescW;
+    const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
+    const double diag = sqrt((double)(W * W + H * H));
+    const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
+    const int side = 2 * radius + 1;
+    for (int i = tid; i < 4 * kDescReps * kDescRepStride; i += 256) S.hist[i] = 0.0;
+    __syncthreads();
+
+    // the reference's rotated-box + image-border test (sift.cpp:645-656)
+    auto accepted = [&](int row, int col) -> bool {
+        const double row_rot = div_sum_w(col * sa + row * ca, hw, ihw);
+        const double col_rot = div_sum_w(col * ca - row * sa, hw, ihw);
+        const double rb = row_rot + kDescW / 2 - 0.5;
+        const double cb = col_rot + kDescW / 2 - 0.5;
+        const int nx = col + x, ny = row + y;
+        return col >= -radius && col <= radius && rb > -1.0 && rb < kDescW && cb > -1.0 &&
+               cb < kDescW && nx > 0 && nx < (W - 1) && ny > 0 && ny < (H - 1);
+    };
+    // this wave's rows are j = wv + 4*m; 64 of them (one per lane) per group
+    for (int g0 = wv; g0 < side; g0 += 4 * 64) {
+        const int j = g0 + 4 * lane;
+        const int row = j - radius;
+        int lo = 0, len = 0;
+        if (j < side && row + y > 0 && row + y < H - 1) {
+            // real-arithmetic interval of |c*sa + row*ca| < 2.5 hw and
+            // |c*ca - row*sa| < 2.5 hw, then snapped with the exact test
+            const double lim = (0.5 * kDescW + 0.5) * hw;
+            double clo = (double)max(-radius, 1 - x), chi = (double)min(radius, W - 2 - x);
+            const double ra = row * ca, rs = row * sa;
+            if (sa != 0.0) {
+                const double a1 = (-lim - ra) / sa, a2 = (lim - ra) / sa;
+                clo = fmax(clo, fmin(a1, a2));
+                chi = fmin(chi, fmax(a1, a2));
+            } else if (!(fabs(ra) < lim)) {
+                chi = clo - 1.0;
+            }
+            if (ca != 0.0) {
+                const double b1 = (-lim + rs) / ca, b2 = (lim + rs) / ca;
+                clo = fmax(clo, fmin(b1, b2));
+                chi = fmin(chi, fmax(b1, b2));
+            } else if (!(fabs(rs) < lim)) {
+                chi = clo - 1.0;
+            }
+            if (clo <= chi + 2.0) {
+                lo = (int)ceil(clo);
+                int hi = (int)floor(chi);
+                for (int t = 0; t < 3 && accepted(row, lo - 1); ++t) --lo;
+                for (int t = 0; t < 3 && lo <= hi + 1 && !accepted(row, lo); ++t) ++lo;
+                for (int t = 0; t < 3 && accepted(row, hi + 1); ++t) ++hi;
+                for (int t = 0; t < 3 && hi >= lo && !accepted(row, hi); ++t) --hi;
+                len = hi >= lo ? hi - lo + 1 : 0;
+            }
+        }
+        // inclusive scan of the row lengths across the wave
+        int pre = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(pre, off);
+            if (lane >= off) pre += t;
+        }
+        const int total = __builtin_amdgcn_readlane(pre, 63);
+        int cur = 0;  // first row (lane index) whose samples are not all consumed
+        for (int t0 = 0; t0 < total; t0 += 64) {
+            const int t = t0 + lane;
+            // row r of sample t: the first r >= cur with pre_r > t
+            int r = cur;
+            int nxt = cur;
+            for (int q = cur; q < 64; ++q) {
+                const int pq = __builtin_amdgcn_readlane(pre, q);
+                if (pq > t0 + 63) break;
+                r += (pq <= t) ? 1 : 0;
+                nxt = q + 1;
+            }
+            const int lo_r = __shfl(lo, r);
+            const int ex_r = __shfl(pre, r) - __shfl(len, r);
+            cur = nxt;
+            if (t < total) {
+                const int srow = g0 + 4 * r - radius;
+                const int scol = lo_r + (t - ex_r);
+                const double row_rot = div_sum_w(scol * sa + srow * ca, hw, ihw);
+                const double col_rot = div_sum_w(scol * ca - srow * sa, hw, ihw);
+                const double rb = row_rot + kDescW / 2 - 0.5;
+                const double cb = col_rot + kDescW / 2 - 0.5;
+                const int nx = scol + x, ny = srow + y;
+                const size_t r0 = (size_t)ny * W;
+                const double dx = img[r0 + nx + 1] - img[r0 + nx - 1];
+                const double dy = img[r0 - W + nx] - img[r0 + W + nx];
+                const double mag = sqrt(dx * dx + dy * dy);
+                double ang = atan2(dy, dx);
+                ang -= pori;
+                // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi:
+                // fmod(a, M) = a - trunc(a/M) M is exact and representable,
+                // so one compare-and-subtract reproduces it bit for bit.
+                if (ang >= kTwoPi) ang -= kTwoPi;
+                else if (ang <= -kTwoPi) ang += kTwoPi;
+                ang += kTwoPi;  // rounded, as in the reference
+                if (ang >= kTwoPi) ang -= kTwoPi;
+                if (ang >= kTwoPi) ang -= kTwoPi;
+                const double ob = ang * bins_per_rad;
+                const double wgt = exp(-(row_rot * row_rot + col_rot * col_rot) / denom);
+                const double m = mag * wgt;
+                const int br = (int)floor(rb), bc = (int)floor(cb), bo = (int)floor(ob);
+                const double fr = rb - br, fc = cb - bc, fo = ob - bo;
+#pragma unroll
+                for (int rq = 0; rq <= 1; ++rq) {
+                    const int ri = br + rq;
+                    if (ri < 0 || ri >= kDescW) continue;
+                    const double vr = m * ((rq == 0) ? 1.0 - fr : fr);
+#pragma unroll
+                    for (int cq = 0; cq <= 1; ++cq) {
+                        const int ci = bc + cq;
+                        if (ci < 0 || ci >= kDescW) continue;
+                        const double vc = vr * ((cq == 0) ? 1.0 - fc : fc);
+#pragma unroll
+                        for (int q = 0; q <= 1; ++q) {
+                            const int oi = (bo + q) % kDescBins;
+                            atomicAdd(&hw_rep[ri * 32 + ci * 8 + oi],
+                                      vc * ((q == 0) ? 1.0 - fo : fo));
+                        }
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    double v = 0.0;
+    if (tid < 128) {
+#pragma unroll
+        for (int r = 0; r < 4 * kDescReps; ++r) v += S.hist[r * kDescRepStride + tid];
+    }
+    // L2 normalise, clamp at DESC_MAGNITUDE_THR, renormalise (sift.cpp:576-603)
+    double sq = v * v;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+    if (lane == 0 && wv < 2) S.red[wv] = sq;
+    __syncthreads();
+    const double ninv = 1.0 / sqrt(S.red[0] + S.red[1]);
+    double cv = v * ninv;
+    if (cv > kMagThr) cv = kMagThr;
+    double sq2 = tid < 128 ? cv * cv : 0.0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) sq2 += __shfl_xor(sq2, off);
+    if (lane == 0 && wv < 2) S.red[2 + wv] = sq2;
+    __syncthreads();
+    if (tid < 128) {
+        const double inv2 = 1.0 / sqrt(S.red[2] + S.red[3]);
+        const double q = floor(kIntFactor * cv * inv2);
+        int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
+        val = val < 0 ? 0 : (val > 255 ? 255 : val);
+        recs[rec].desc[tid] = (uint8_t)val;
+        if (desc_f32) desc_f32[(size_t)rec * 128 + tid] = (float)(cv * inv2);
+        if (rec < ex.cap) {
+            ex.rec[rec].desc[tid] = (uint8_t)val;
+            if (tid == 0) {
+                sift_kp& r = ex.rec[rec];
+                r.x = kx;
+                r.y = ky;
+                r.octave = o;
+                r.layer = layer;
+                r.size = ksize;
+                r.pori = pori;
+                ex.off0[rec] = off0;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_orient_describe(
+    const PyrTable* __restrict__ pt, DevParams P, const RawKp* __restrict__ raw,
+    const unsigned* __restrict__ raw_begin, const unsigned* __restrict__ n_raw, unsigned cap_raw,
+    sift_kp* __restrict__ recs, double* __restrict__ rec_off0,
+    const unsigned* __restrict__ rec_begin, unsigned* __restrict__ n_rec, unsigned cap_rec,
+    float* __restrict__ desc_f32, unsigned* __restrict__ work, ExportSink ex) {
+    __shared__ KpLds S;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const unsigned n = min(*n_raw, cap_raw);
     const unsigned k0 = min(*raw_begin, n);
     const int nb = P.num_bins;
     const int stride = nb + 2;  // pad rotates LDS banks between replicas
-    double* rep = &hist[(wv * kOriReps + (lane & (kOriReps - 1))) * stride];
+    double* rep = &S.hist[(wv * kOriReps + (lane & (kOriReps - 1))) * stride];
     for (;;) {
-        if (tid == 0) s_k = k0 + atomicAdd(work, 1u);
+        if (tid == 0) {
+            S.k = k0 + atomicAdd(work, 1u);
+            S.npk = 0;
+        }
         __syncthreads();
-        const unsigned k = s_k;
+        const unsigned k = S.k;
         if (k >= n) break;
         const RawKp kp = raw[k];
         const int o = kp.octave;
@@ -726,7 +1003,7 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
         gdouble* img = gbl(pt->lvl[o][kp.layer]);
         const int W = pt->w[o], H = pt->h[o];
         const int side = 2 * radius + 1;
-        for (int i = tid; i < 4 * kOriReps * stride; i += 256) hist[i] = 0.0;
+        for (int i = tid; i < 4 * kOriReps * stride; i += 256) S.hist[i] = 0.0;
         __syncthreads();
         // window rows j (y offset) by chunks of 64 columns i (x offset)
         const int cpr = (side + 63) >> 6;  // chunks per row
@@ -751,22 +1028,22 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
         __syncthreads();
         for (int b = tid; b < nb; b += 256) {
             double v = 0.0;
-            for (int r = 0; r < 4 * kOriReps; ++r) v += hist[r * stride + b];
-            hs[b] = v;
+            for (int r = 0; r < 4 * kOriReps; ++r) v += S.hist[r * stride + b];
+            S.hs[b] = v;
         }
         __syncthreads();
         if (tid == 0) {
             for (int it = 0; it < kSmoothIters; ++it) {
-                double prev = hs[nb - 1];  // h[i-1] for i = 0: not yet updated
-                const double h0_old = hs[0];
+                double prev = S.hs[nb - 1];  // h[i-1] for i = 0: not yet updated
+                const double h0_old = S.hs[0];
                 double first_new = 0.0;
                 for (int i = 0; i < nb; ++i) {
-                    const double h1 = hs[i];
+                    const double h1 = S.hs[i];
                     // h[i+1]: old value, except for i = nb-1 where it is the
                     // already-updated h[0] (and h[0] itself when nb == 1)
-                    const double h2 = (i + 1 < nb) ? hs[i + 1] : (i == 0 ? h0_old : first_new);
+                    const double h2 = (i + 1 < nb) ? S.hs[i + 1] : (i == 0 ? h0_old : first_new);
                     const double v = 0.25 * prev + 0.5 * h1 + 0.25 * h2;
-                    hs[i] = v;
+                    S.hs[i] = v;
                     prev = v;
                     if (i == 0) first_new = v;
                 }
@@ -775,277 +1052,58 @@ __global__ __launch_bounds__(256) void k_orient(const PyrTable* __restrict__ pt,
         __syncthreads();
         // max over bins (histogram entries are >= 0): every wave reduces all
         double mx = 0.0;
-        for (int b = lane; b < nb; b += 64) mx = fmax(mx, hs[b]);
+        for (int b = lane; b < nb; b += 64) mx = fmax(mx, S.hs[b]);
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
         for (int i = tid; i < nb; i += 256) {
-            const double h0 = hs[i == 0 ? nb - 1 : i - 1];
-            const double h1 = hs[i];
-            const double h2 = hs[i + 1 == nb ? 0 : i + 1];
+            const double h0 = S.hs[i == 0 ? nb - 1 : i - 1];
+            const double h1 = S.hs[i];
+            const double h2 = S.hs[i + 1 == nb ? 0 : i + 1];
             if (h1 > h0 && h1 > h2 && h1 > (P.peak_ratio * mx)) {
                 double fi = i + 0.5 * (h0 - h2) / (h0 - 2 * h1 + h2);
                 fi = fmod(fi + nb, (double)nb);
                 double ori = kTwoPi * fi / nb;
                 ori = fmod(ori + kTwoPi, kTwoPi);
-                const unsigned idx = atomicAdd(n_out, 1u);
-                if (idx < cap_out) {
-                    double rx = kp.x, ry = kp.y, rs = kp.size;
-                    if (P.double_image) {
-                        rx /= 2;
-                        ry /= 2;
-                        rs /= 2;
-                    }
-                    out[idx].x = rx;
-                    out[idx].y = ry;
-                    out[idx].octave = kp.octave;
-                    out[idx].layer = kp.layer;
-                    out[idx].size = rs;
-                    out[idx].pori = ori;
-                    out_off0[idx] = kp.off0;
-                }
+                S.pk[atomicAdd(&S.npk, 1u)] = ori;
             }
         }
         __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_descriptor: compute_descriptors + update_histogram + convert_hist_to_desc
-// (sift.cpp:541-682), one 256-thread workgroup per oriented keypoint, taken
-// from a work counter (persistent grid, dynamic balance over keypoints of
-// very different window sizes).
-//  * Accepted samples are enumerated, not searched: for a fixed row, the
-//    reference's test (sift.cpp:651-656) is a conjunction of conditions that
-//    are each monotone in col (col*sin, col*cos, the division and the +1.5
-//    are monotone in IEEE arithmetic), so the accepted columns form one
-//    interval. Each lane estimates the interval of one row analytically and
-//    snaps both ends with the exact test; a wave scan of the lengths then maps
-//    64 consecutive accepted samples to (row, col) per step, so every lane
-//    always works on an accepted sample.
-//  * Rows are dealt round-robin to the four waves; each wave adds into its
-//    own four lane-interleaved replicas of the 4x4x8 f64 histogram
-//    (ds_add_f64; replicas cut same-address serialisation 4x), summed in a
-//    fixed order at the end, so results are reproducible run to run.
-//  * /hist_width is a correctly rounded division by a per-keypoint constant
-//    (div_sum_w with inv = 1/hist_width), the fmods of sift.cpp:667 reduce
-//    exactly to compare-and-subtract (|angle| < 2*2pi, fmod is exact).
-//  * The two normalisation sums run sequentially on one lane in index order.
-// ---------------------------------------------------------------------------
-constexpr int kDescReps = 4;          // histogram replicas per wave
-constexpr int kDescRepStride = 130;   // doubles; the pad rotates LDS banks
-
-__global__ __launch_bounds__(256) void k_descriptor(const PyrTable* __restrict__ pt,
-                                                    DevParams P, sift_kp* __restrict__ recs,
-                                                    const unsigned* __restrict__ rec_begin,
-                                                    const unsigned* __restrict__ n_p,
-                                                    unsigned cap, float* __restrict__ desc_f32,
-                                                    unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ double hist[4][kDescReps * kDescRepStride];
-    __shared__ double hsum[128];
-    __shared__ double s_inv;
-    __shared__ unsigned s_k;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const unsigned n = min(*n_p, cap);
-    const unsigned k0 = min(*rec_begin, n);
-    if (ex.cnt && blockIdx.x == 0 && tid == 0) {
-        ex.cnt[0] = k0;
-        ex.cnt[1] = n;
-    }
-    double* hw_rep = &hist[wv][(lane & (kDescReps - 1)) * kDescRepStride];
-    for (;;) {
-        if (tid == 0) s_k = k0 + atomicAdd(work, 1u);
-        __syncthreads();
-        const unsigned k = s_k;
-        if (k >= n) break;
-        const double* hdr = reinterpret_cast<const double*>(&recs[k]);
-        const double kx = hdr[0], ky = hdr[1];
-        const int o = reinterpret_cast<const int*>(hdr)[4];
-        const int layer = reinterpret_cast<const int*>(hdr)[5];
-        const double ksize = hdr[3], pori = hdr[4];
-        gdouble* img = gbl(pt->lvl[o][layer]);
-        const int W = pt->w[o], H = pt->h[o];
-        const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
-        const int x = (int)(kx * inv);
-        const int y = (int)(ky * inv);
-        const double size = ksize * inv;
-        const double bins_per_rad = kDescBins / kTwoPi;
-        const double ca = cos(pori), sa = sin(pori);
-        const double hw = P.desc_scale_factor * size;
-        const double ihw = 1.0 / hw;
-        const double denom = 0.5 * kDescW * kDescW;
-        const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
-        const double diag = sqrt((double)(W * W + H * H));
-        const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
-        const int side = 2 * radius + 1;
-        for (int i = lane; i < kDescReps * kDescRepStride; i += 64) hist[wv][i] = 0.0;
-        wave_sync();
-
-        // the reference's rotated-box + image-border test (sift.cpp:645-656)
-        auto accepted = [&](int row, int col) -> bool {
-            const double row_rot = div_sum_w(col * sa + row * ca, hw, ihw);
-            const double col_rot = div_sum_w(col * ca - row * sa, hw, ihw);
-            const double rb = row_rot + kDescW / 2 - 0.5;
-            const double cb = col_rot + kDescW / 2 - 0.5;
-            const int nx = col + x, ny = row + y;
-            return col >= -radius && col <= radius && rb > -1.0 && rb < kDescW && cb > -1.0 &&
-                   cb < kDescW && nx > 0 && nx < (W - 1) && ny > 0 && ny < (H - 1);
-        };
-        // this wave's rows are j = wv + 4*m; 64 of them (one per lane) per group
-        for (int g0 = wv; g0 < side; g0 += 4 * 64) {
-            const int j = g0 + 4 * lane;
-            const int row = j - radius;
-            int lo = 0, len = 0;
-            if (j < side && row + y > 0 && row + y < H - 1) {
-                // real-arithmetic interval of |c*sa + row*ca| < 2.5 hw and
-                // |c*ca - row*sa| < 2.5 hw, then snapped with the exact test
-                const double lim = (0.5 * kDescW + 0.5) * hw;
-                double clo = (double)max(-radius, 1 - x), chi = (double)min(radius, W - 2 - x);
-                const double ra = row * ca, rs = row * sa;
-                if (sa != 0.0) {
-                    const double a1 = (-lim - ra) / sa, a2 = (lim - ra) / sa;
-                    clo = fmax(clo, fmin(a1, a2));
-                    chi = fmin(chi, fmax(a1, a2));
-                } else if (!(fabs(ra) < lim)) {
-                    chi = clo - 1.0;
-                }
-                if (ca != 0.0) {
-                    const double b1 = (-lim + rs) / ca, b2 = (lim + rs) / ca;
-                    clo = fmax(clo, fmin(b1, b2));
-                    chi = fmin(chi, fmax(b1, b2));
-                } else if (!(fabs(rs) < lim)) {
-                    chi = clo - 1.0;
-                }
-                if (clo <= chi + 2.0) {
-                    lo = (int)ceil(clo);
-                    int hi = (int)floor(chi);
-                    for (int t = 0; t < 3 && accepted(row, lo - 1); ++t) --lo;
-                    for (int t = 0; t < 3 && lo <= hi + 1 && !accepted(row, lo); ++t) ++lo;
-                    for (int t = 0; t < 3 && accepted(row, hi + 1); ++t) ++hi;
-                    for (int t = 0; t < 3 && hi >= lo && !accepted(row, hi); ++t) --hi;
-                    len = hi >= lo ? hi - lo + 1 : 0;
-                }
-            }
-            // inclusive scan of the row lengths across the wave
-            int pre = len;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int t = __shfl_up(pre, off);
-                if (lane >= off) pre += t;
-            }
-            const int total = __builtin_amdgcn_readlane(pre, 63);
-            int cur = 0;  // first row (lane index) whose samples are not all consumed
-            for (int t0 = 0; t0 < total; t0 += 64) {
-                const int t = t0 + lane;
-                // row r of sample t: the first r >= cur with pre_r > t
-                int r = cur;
-                int nxt = cur;
-                for (int q = cur; q < 64; ++q) {
-                    const int pq = __builtin_amdgcn_readlane(pre, q);
-                    if (pq > t0 + 63) break;
-                    r += (pq <= t) ? 1 : 0;
-                    nxt = q + 1;
-                }
-                const int lo_r = __shfl(lo, r);
-                const int ex_r = __shfl(pre, r) - __shfl(len, r);
-                cur = nxt;
-                if (t < total) {
-                    const int srow = g0 + 4 * r - radius;
-                    const int scol = lo_r + (t - ex_r);
-                    const double row_rot = div_sum_w(scol * sa + srow * ca, hw, ihw);
-                    const double col_rot = div_sum_w(scol * ca - srow * sa, hw, ihw);
-                    const double rb = row_rot + kDescW / 2 - 0.5;
-                    const double cb = col_rot + kDescW / 2 - 0.5;
-                    const int nx = scol + x, ny = srow + y;
-                    const size_t r0 = (size_t)ny * W;
-                    const double dx = img[r0 + nx + 1] - img[r0 + nx - 1];
-                    const double dy = img[r0 - W + nx] - img[r0 + W + nx];
-                    const double mag = sqrt(dx * dx + dy * dy);
-                    double ang = atan2(dy, dx);
-                    ang -= pori;
-                    // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi:
-                    // fmod(a, M) = a - trunc(a/M) M is exact and representable,
-                    // so one compare-and-subtract reproduces it bit for bit.
-                    if (ang >= kTwoPi) ang -= kTwoPi;
-                    else if (ang <= -kTwoPi) ang += kTwoPi;
-                    ang += kTwoPi;  // rounded, as in the reference
-                    if (ang >= kTwoPi) ang -= kTwoPi;
-                    if (ang >= kTwoPi) ang -= kTwoPi;
-                    const double ob = ang * bins_per_rad;
-                    const double wgt = exp(-(row_rot * row_rot + col_rot * col_rot) / denom);
-                    const double m = mag * wgt;
-                    const int br = (int)floor(rb), bc = (int)floor(cb), bo = (int)floor(ob);
-                    const double fr = rb - br, fc = cb - bc, fo = ob - bo;
-#pragma unroll
-                    for (int rq = 0; rq <= 1; ++rq) {
-                        const int ri = br + rq;
-                        if (ri < 0 || ri >= kDescW) continue;
-                        const double vr = m * ((rq == 0) ? 1.0 - fr : fr);
-#pragma unroll
-                        for (int cq = 0; cq <= 1; ++cq) {
-                            const int ci = bc + cq;
-                            if (ci < 0 || ci >= kDescW) continue;
-                            const double vc = vr * ((cq == 0) ? 1.0 - fc : fc);
-#pragma unroll
-                            for (int q = 0; q <= 1; ++q) {
-                                const int oi = (bo + q) % kDescBins;
-                                atomicAdd(&hw_rep[ri * 32 + ci * 8 + oi],
-                                          vc * ((q == 0) ? 1.0 - fo : fo));
-                            }
-                        }
-                    }
-                }
-            }
+        const unsigned npk = S.npk;
+        double rx = kp.x, ry = kp.y, rs = kp.size;
+        if (P.double_image) {  // sift.cpp:522-526
+            rx /= 2;
+            ry /= 2;
+            rs /= 2;
         }
-        __syncthreads();
-        if (tid < 128) {
-            double v = 0.0;
-#pragma unroll
-            for (int w = 0; w < 4; ++w)
-#pragma unroll
-                for (int r = 0; r < kDescReps; ++r) v += hist[w][r * kDescRepStride + tid];
-            hsum[tid] = v;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            double norm = 0.0;
-            for (int i = 0; i < 128; ++i) norm += hsum[i] * hsum[i];
-            norm = sqrt(norm);
-            double ninv = 1.0 / norm;
-            norm = 0.0;
-            for (int i = 0; i < 128; ++i) {
-                double v = hsum[i] * ninv;
-                if (v > kMagThr) v = kMagThr;
-                hsum[i] = v;
-                norm += v * v;
-            }
-            norm = sqrt(norm);
-            s_inv = 1.0 / norm;
-        }
-        __syncthreads();
-        if (tid < 128) {
-            const double ninv = s_inv;
-            const double hv = hsum[tid];
-            const double q = floor(kIntFactor * hv * ninv);
-            int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
-            val = val < 0 ? 0 : (val > 255 ? 255 : val);
-            recs[k].desc[tid] = (uint8_t)val;
-            if (desc_f32) desc_f32[(size_t)k * 128 + tid] = (float)(hv * ninv);
-            if (k < ex.cap) {
-                ex.rec[k].desc[tid] = (uint8_t)val;
+        for (unsigned p = 0; p < npk; ++p) {
+            const double ori = S.pk[p];
+            if (tid == 0) S.rec = atomicAdd(n_rec, 1u);
+            __syncthreads();
+            const unsigned rec = S.rec;
+            if (rec < cap_rec) {
                 if (tid == 0) {
-                    sift_kp& r = ex.rec[k];
-                    r.x = kx;
-                    r.y = ky;
-                    r.octave = o;
-                    r.layer = layer;
-                    r.size = ksize;
-                    r.pori = pori;
-                    ex.off0[k] = ex.off0_src[k];
+                    sift_kp& r = recs[rec];
+                    r.x = rx;
+                    r.y = ry;
+                    r.octave = kp.octave;
+                    r.layer = kp.layer;
+                    r.size = rs;
+                    r.pori = ori;
+                    rec_off0[rec] = kp.off0;
                 }
+                describe(S, pt, P, recs, rec, rx, ry, kp.octave, kp.layer, rs, ori, kp.off0,
+                         desc_f32, ex);
             }
+            __syncthreads();
         }
-        __syncthreads();
+    }
+    // the last workgroup to finish publishes this launch's record range
+    if (ex.cnt && tid == 0) {
+        __threadfence();
+        if (atomicAdd(work + 1, 1u) == gridDim.x - 1) {
+            ex.cnt[0] = *rec_begin;
+            ex.cnt[1] = atomicAdd(n_rec, 0u);
+        }
     }
 }
 
@@ -1182,14 +1240,15 @@ hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double
 
 hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
                                 int thr, sift_extremum* out, unsigned* counter, unsigned cap,
-                                hipStream_t s) {
+                                const DevParams& P, RawKp* raw, unsigned* n_raw,
+                                unsigned cap_raw, hipStream_t s) {
     const int blocks = eg.first_tile[eg.n];
     if (blocks == 0) return hipSuccess;
     switch (n_gauss) {
 #define SIFT_EXT_CASE(NL)                                                                 \
     case NL:                                                                              \
         hipLaunchKernelGGL((k_extrema_tiles<NL>), dim3(blocks), dim3(256), 0, s, d_pt, eg, \
-                           thr, out, counter, cap);                                       \
+                           thr, out, counter, cap, P, raw, n_raw, cap_raw);               \
         return hipGetLastError();
         SIFT_EXT_CASE(4)
         SIFT_EXT_CASE(5)
@@ -1236,27 +1295,18 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
     return hipGetLastError();
 }
 
-hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
-                         const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
-                         sift_kp* out, double* out_off0, unsigned* n_out, unsigned cap_out,
-                         unsigned* work, hipStream_t s) {
-    // persistent: workgroups pull keypoints from the work counter
-    unsigned blocks = 1024;
-    if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
-    hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin, n_raw,
-                       cap_raw, out, out_off0, n_out, cap_out, work);
-    return hipGetLastError();
-}
-
-hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
-                             const unsigned* rec_begin, const unsigned* n, unsigned cap,
-                             float* desc_f32, unsigned* work, const ExportSink& ex,
-                             hipStream_t s) {
+hipError_t launch_orient_describe(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
+                                  const unsigned* raw_begin, const unsigned* n_raw,
+                                  unsigned cap_raw, sift_kp* recs, double* rec_off0,
+                                  const unsigned* rec_begin, unsigned* n_rec, unsigned cap_rec,
+                                  float* desc_f32, unsigned* work, const ExportSink& ex,
+                                  hipStream_t s) {
     // persistent: 4 workgroups per CU pull keypoints from the work counter
     unsigned blocks = 1024;
-    if (blocks > cap) blocks = cap > 0 ? cap : 1;
-    hipLaunchKernelGGL(k_descriptor, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_begin, n,
-                       cap, desc_f32, work, ex);
+    if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
+    hipLaunchKernelGGL(k_orient_describe, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin,
+                       n_raw, cap_raw, recs, rec_off0, rec_begin, n_rec, cap_rec, desc_f32, work,
+                       ex);
     return hipGetLastError();
 }
 

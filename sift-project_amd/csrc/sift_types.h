@@ -91,7 +91,7 @@ struct RawKp {
     int octave, layer;
 };
 
-// Where k_descriptor also writes each finished record (mapped, coherent
+// Where k_orient_describe also writes each finished record (mapped, coherent
 // pinned host memory), so the host can finalise a keypoint batch while the
 // device works on the next: rec/off0 index = record index (< cap), cnt =
 // this launch's [begin, end) record range.
@@ -99,7 +99,6 @@ struct ExportSink {
     sift_kp* rec;
     double* off0;
     unsigned* cnt;
-    const double* off0_src;
     unsigned cap;
 };
 
