@@ -30,12 +30,12 @@ namespace {
 
 // device counter block: [0..3] live counters (candidates, refined, oriented),
 // [4..7] zeros, then per keypoint batch g a 4-word snapshot taken after its
-// extrema (the batch's candidate end and its record begins), then two
-// keypoint work counters per chain (orientation, descriptor)
+// extrema (the batch's candidate end and its record begins), then four
+// words per chain: work and done counters of orientation and descriptor
 constexpr int kCtrZeros = 4;
 constexpr int kCtrSnap = 8;
 constexpr int kCtrWork = kCtrSnap + 4 * (kMaxOctaves + 1);
-constexpr int kCtrWords = kCtrWork + 2 * (kMaxOctaves + 2);
+constexpr int kCtrWords = kCtrWork + 4 * (kMaxOctaves + 2);
 
 template <class T>
 struct Pinned {  // grow-only pinned host buffer (fast async D2H, no staging)
@@ -104,6 +104,11 @@ struct sift_ctx {
     hipStream_t stream = nullptr;   // A: pyramid
     hipStream_t stream2 = nullptr;  // B: odd octaves of the pyramid
     hipStream_t stream3 = nullptr;  // C: extrema, refine, orientation, descriptor
+    // persistent workgroups of orientation / descriptor: 768 = what fits at
+    // once (3 per CU at the descriptor's 168 VGPRs); measured best of
+    // 512/768/1024 (CU-masking stream C was measured slower)
+    unsigned kp_wgs = 768;
+    int batch_px_log2 = 20;         // octaves of >= 2^this pixels get their own batch
     std::vector<hipEvent_t> sync_ev;
 
     double* d_in = nullptr;
@@ -339,16 +344,15 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             break;
         }
     const bool tiles = p->window_size / 2 == 1;
-    // Keypoint batches on stream C: each large octave (>= kBatchPx pixels) is
+    // Keypoint batches on stream C: each large octave (>= batch_px pixels) is
     // its own batch as soon as its levels exist; the smaller ones, whose
     // keypoint work is too small to amortise a chain of launches, form one
-    // final batch. A batch: counter snapshot (its candidate / record begins),
-    // extrema (window 3: with the refine fused in), then orientation +
-    // descriptor of the refined keypoints it appended.
-    constexpr size_t kBatchPx = (size_t)1 << 20;
+    // final batch. A batch: extrema, a counter snapshot (its candidate end,
+    // raw / record begins), refine, orientation, descriptor.
+    const size_t batch_px = (size_t)1 << ctx->batch_px_log2;
     int o_merge = g.octaves;  // first octave of the final batch
     for (int o = 0; o < g.octaves; ++o)
-        if ((size_t)g.W[o] * g.H[o] < kBatchPx) {
+        if ((size_t)g.W[o] * g.H[o] < batch_px) {
             o_merge = o;
             break;
         }
@@ -358,8 +362,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         if (tiles) {
             const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
             SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
-                                              ctx->d_ctr + 0, ctx->cap_cand, dp, ctx->d_raw,
-                                              ctx->d_ctr + 1, ctx->cap_raw, sC));
+                                              ctx->d_ctr + 0, ctx->cap_cand, sC));
         } else {
             for (int o = o_begin; o < o_end; ++o)
                 SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
@@ -378,14 +381,14 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     // poison: a range no launch published reads as "not exported"
     std::fill(ctx->exp_cnt.h, ctx->exp_cnt.h + ctx->exp_cnt.cap, 0xFFFFFFFFu);
     int n_chains = 0;
-    // extrema over [o_begin, o_end) then the keypoint chain. `begin` is a
-    // counter snapshot: taken before the extrema when the refine is fused
-    // (window 3: raw/record begins), after them otherwise (this batch's
-    // candidate end, the next batch's cand_begin), before the refine.
-    auto run_chain = [&](int o_begin, int o_end, const unsigned* cand_begin, unsigned* begin,
-                         bool fused) -> int {
+    // extrema over [o_begin, o_end) then refine -> orientation -> descriptor.
+    // `begin` (a counter snapshot taken right after the extrema) holds this
+    // batch's candidate end and its raw / record begins; candidates start at
+    // cand_begin (the previous batch's snapshot). The re-run passes nullptr.
+    auto run_chain = [&](int o_begin, int o_end, const unsigned* cand_begin,
+                         unsigned* begin) -> int {
         const int ci = n_chains++;
-        unsigned* work = ctx->d_ctr + kCtrWork + 2 * ci;
+        unsigned* work = ctx->d_ctr + kCtrWork + 4 * ci;
         while ((int)ctx->chain_ev.size() <= ci) {
             hipEvent_t e;
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
@@ -394,20 +397,19 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         }
         const ExportSink ex{ctx->exp_rec.d, ctx->exp_off0.d, ctx->exp_cnt.d + 2 * ci,
                             (unsigned)ctx->exp_rec.cap};
-        if (fused && begin) SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
         int st2 = launch_extrema_range(o_begin, o_end);
         if (st2 != SIFT_OK) return st2;
-        if (!fused) {
-            if (begin) SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
-            SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin, ctx->d_ctr + 0,
-                                       ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw,
-                                       sC));
-        }
+        if (begin) SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
         const unsigned* b = begin ? begin : zeros;
-        SIFT_HIP_TRY(launch_orient_describe(ctx->d_pt, dp, ctx->d_raw, b + 1, ctx->d_ctr + 1,
-                                            ctx->cap_raw, ctx->d_ori, ctx->d_off0, b + 2,
-                                            ctx->d_ctr + 2, ctx->cap_ori,
-                                            out_desc_f32 ? ctx->d_df32 : nullptr, work, ex, sC));
+        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin, ctx->d_ctr + 0,
+                                   ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, sC));
+        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, b + 1, ctx->d_ctr + 1, ctx->cap_raw,
+                                   ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2, ctx->cap_ori, work,
+                                   ctx->kp_wgs, sC));
+        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, ctx->d_off0, b + 2,
+                                       ctx->d_ctr + 2, ctx->cap_ori,
+                                       out_desc_f32 ? ctx->d_df32 : nullptr, work + 2, ex,
+                                       ctx->kp_wgs, sC));
         SIFT_HIP_TRY(hipEventRecord(ctx->chain_ev[ci], sC));
         return SIFT_OK;
     };
@@ -421,7 +423,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
             SIFT_HIP_TRY(hipStreamWaitEvent(sC, pyr_done, 0));
         }
-        return run_chain(o_begin, o_end, gb == 0 ? zeros : snap(gb - 1), snap(gb), tiles);
+        return run_chain(o_begin, o_end, gb == 0 ? zeros : snap(gb - 1), snap(gb));
     };
     // The pyramid alternates between two streams, octave o on pyr[o % 2]:
     // octave o+1 only needs the decimated level `intervals` of octave o, so it
@@ -501,7 +503,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
             SIFT_HIP_TRY(hipStreamSynchronize(sC));
             n_chains = 0;
-            if ((st = run_chain(0, g.octaves, zeros, nullptr, tiles)) != SIFT_OK) return st;
+            if ((st = run_chain(0, g.octaves, zeros, nullptr)) != SIFT_OK) return st;
             SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
         }
@@ -649,6 +651,10 @@ int sift_hip_create(int device, sift_ctx** out) {
     ctx->device = device;
     int prio_lo = 0, prio_hi = 0;  // numerically lower = higher priority
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+    if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::atoi(e);
+    if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
+    if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) ctx->batch_px_log2 = std::atoi(e);
+    if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 20;
     if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess ||

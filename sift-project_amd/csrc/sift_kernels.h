@@ -31,11 +31,9 @@ bool launch_blur_initial_fused(const double* in, int w, int h, int c, int dbl, d
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
                               const BlurTaps* d_taps, hipStream_t s, hipEvent_t e0,
                               hipEvent_t e1);
-// with raw != nullptr every candidate is also refined in place (RawKp list)
 hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
                                 int thr, sift_extremum* out, unsigned* counter, unsigned cap,
-                                const DevParams& P, RawKp* raw, unsigned* n_raw,
-                                unsigned cap_raw, hipStream_t s);
+                                hipStream_t s);
 hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
                               int window_size, int thr, sift_extremum* out, unsigned* counter,
                               unsigned cap, hipStream_t s);
@@ -45,14 +43,18 @@ hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s);
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s);
-// orientation + descriptor of raw keypoints [*raw_begin, *n_raw): records
-// appended at n_rec (from *rec_begin); `work`: two zeroed device words (work
-// counter, done counter); ex.cnt receives the launch's record range.
-hipError_t launch_orient_describe(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
-                                  const unsigned* raw_begin, const unsigned* n_raw,
-                                  unsigned cap_raw, sift_kp* recs, double* rec_off0,
-                                  const unsigned* rec_begin, unsigned* n_rec, unsigned cap_rec,
-                                  float* desc_f32, unsigned* work, const ExportSink& ex,
-                                  hipStream_t s);
+// orientation of raw keypoints [*raw_begin, *n_raw) -> records appended at
+// n_rec; descriptors of records [*rec_begin, *n_rec). `work`: two zeroed
+// device words per launch (work counter, done counter); ex.cnt receives the
+// descriptor launch's record range.
+hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
+                         const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
+                         sift_kp* recs, double* rec_off0, unsigned* n_rec, unsigned cap_rec,
+                         unsigned* work, unsigned wgs, hipStream_t s);
+hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
+                             const double* rec_off0, const unsigned* rec_begin,
+                             const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
+                             unsigned* work, const ExportSink& ex, unsigned wgs,
+                             hipStream_t s);
 
 }  // namespace sift_amd

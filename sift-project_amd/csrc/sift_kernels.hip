@@ -472,9 +472,6 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
         dec[(size_t)(y >> 1) * Wd + (x >> 1)] = o;
 }
 
-__device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, int ex, int ey,
-                           int ez, int o, RawKp* out);
-
 // ---------------------------------------------------------------------------
 // Extrema: detect_octave_extrema + is_extremum (sift.cpp:227-291). A pixel is
 // kept iff |D_z| > threshold (the int threshold of sift.cpp:266,279) and it
@@ -489,18 +486,16 @@ __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, 
 // memory round trip), then each thread takes one column x four centre rows
 // and walks the layers with a rolling window of three layers' 3x3 max/min
 // in registers. Candidates are compacted with a 64-bit ballot per
-// (row, layer) and one atomic per wave. When `raw` is set, every candidate is
-// refined (compute_keypoints, sift.cpp:330-436) by the thread that found it,
-// right after the scan (no separate launch; the tile's pixels are L2-hot).
+// (row, layer) and one atomic per wave. (Refining each candidate right here
+// was measured slower: the refine's dependent 27-point gathers serialise in
+// the tile's workgroup, where the separate thread-per-candidate k_refine
+// overlaps them across all candidates.)
 template <int NL>
 __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restrict__ pt,
                                                        ExtremaGrid eg, int thr,
                                                        sift_extremum* __restrict__ out,
                                                        unsigned* __restrict__ counter,
-                                                       unsigned cap, DevParams P,
-                                                       RawKp* __restrict__ raw,
-                                                       unsigned* __restrict__ n_raw,
-                                                       unsigned cap_raw) {
+                                                       unsigned cap) {
     constexpr int ND = NL - 1;
     constexpr int TW = 64, TH = 16, SW = TW + 2, SH = TH + 2;
     constexpr int NPIX = SW * SH;             // 1188 staged pixels
@@ -539,7 +534,6 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
     const int r0 = (tid >> 6) * 4;   // first of this thread's four centre rows
     const int x = cx0 + c;
     const double dthr = (double)thr;
-    uint64_t mine = 0;  // this thread's candidates: bit 4*(z-1) + row k
     // rolling 3x3 max/min of layers l-2 (p), l-1 (q), l (n) for 4 centres
     double pmx[4], pmn[4], qmx[4], qmn[4];
 #pragma unroll
@@ -576,7 +570,6 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
                     const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
                     if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, o};
                 }
-                if (cand) mine |= 1ull << (4 * (z - 1) + k);
             }
         }
 #pragma unroll
@@ -585,17 +578,6 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
             pmn[k] = qmn[k];
             qmx[k] = nmx[k];
             qmn[k] = nmn[k];
-        }
-    }
-    if (raw) {
-        while (mine) {
-            const int bit = __builtin_ctzll(mine);
-            mine &= mine - 1;
-            RawKp r;
-            if (refine_one(pt, P, x, cy0 + r0 + (bit & 3), (bit >> 2) + 1, o, &r)) {
-                const unsigned idx = atomicAdd(n_raw, 1u);
-                if (idx < cap_raw) raw[idx] = r;
-            }
         }
     }
 }
@@ -633,9 +615,7 @@ __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict_
 // refine_one: compute_keypoints (sift.cpp:330-436) for one candidate, with
 // get_pixel_cube, compute_gradient, compute_hessian, fit_quadratic
 // (sift.cpp:32-106); bit-exact (no libm except the size's pow(2, t), which
-// the host recomputes with glibc for the final records). Called from the
-// extrema kernel right where a candidate is found (window_size 3) and from
-// k_refine (other window sizes).
+// the host recomputes with glibc for the final records).
 // ---------------------------------------------------------------------------
 __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, int ex, int ey,
                            int ez, int o, RawKp* out) {
@@ -709,8 +689,8 @@ __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, 
     return true;
 }
 
-// Candidates [cand_begin, n_cand) of the generic-window extrema path, one
-// thread each.
+// k_refine: candidates [cand_begin, n_cand), one thread each (the dependent
+// gathers of all candidates in flight together).
 __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt, DevParams P,
                                                 const sift_extremum* __restrict__ cand,
                                                 const unsigned* __restrict__ cand_begin,
@@ -731,14 +711,15 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
 }
 
 // ---------------------------------------------------------------------------
-// k_orient_describe: compute_orientations (sift.cpp:447-533) and, for every
-// orientation peak, compute_descriptors + update_histogram +
-// convert_hist_to_desc (sift.cpp:541-682) of the keypoint it makes; one
-// 256-thread workgroup per refined keypoint, taken from a work counter
-// (persistent grid: dynamic balance over windows of very different sizes).
-// Describing every oriented keypoint before clean_keypoints (sift.cpp:762,
-// host) gives the same final records: std::unique only drops records equal
-// in (x, y, size, pori), and the kept one is described from its own fields.
+// k_orient: compute_orientations (sift.cpp:447-533), one record per
+// orientation peak; k_descriptor: compute_descriptors + update_histogram +
+// convert_hist_to_desc (sift.cpp:541-682) of every record. Both take one
+// 256-thread workgroup per keypoint from a work counter (persistent grid:
+// dynamic balance over windows of very different sizes). Describing every
+// oriented keypoint before clean_keypoints (sift.cpp:762, host) gives the
+// same final records: std::unique only drops records equal in (x, y, size,
+// pori), and the kept one is described from its own fields. (One fused
+// orientation+descriptor kernel was measured slower: 242 VGPRs, 2 waves/SIMD.)
 //
 // Orientation
 //  * The (2r+1)^2 window is swept 256 samples at a time (lanes along x, so
@@ -864,7 +845,9 @@ __device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevPar
         }
         const int total = __builtin_amdgcn_readlane(pre, 63);
         int cur = 0;  // first row (lane index) whose samples are not all consumed
-        for (int t0 = 0; t0 < total; t0 += 64) {
+        // (row, col) of sample t0 + lane; false past the end. Wave-uniform
+        // call sites only (shuffles); advances the row cursor.
+        auto locate = [&](int t0, int& srow, int& scol) -> bool {
             const int t = t0 + lane;
             // row r of sample t: the first r >= cur with pre_r > t
             int r = cur;
@@ -878,17 +861,37 @@ __device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevPar
             const int lo_r = __shfl(lo, r);
             const int ex_r = __shfl(pre, r) - __shfl(len, r);
             cur = nxt;
-            if (t < total) {
-                const int srow = g0 + 4 * r - radius;
-                const int scol = lo_r + (t - ex_r);
+            srow = g0 + 4 * r - radius;
+            scol = lo_r + (t - ex_r);
+            return t < total;
+        };
+        auto fetch = [&](bool ok, int srow, int scol, double* v) {
+            if (ok) {
+                const size_t r0 = (size_t)(srow + y) * W + scol + x;
+                v[0] = img[r0 + 1];
+                v[1] = img[r0 - 1];
+                v[2] = img[r0 - W];
+                v[3] = img[r0 + W];
+            }
+        };
+        // one sample ahead: the next sample's four gradient loads are in
+        // flight while the current one is processed
+        int srow = 0, scol = 0;
+        double cv[4] = {0.0, 0.0, 0.0, 0.0}, nv[4] = {0.0, 0.0, 0.0, 0.0};
+        bool cok = total > 0 && locate(0, srow, scol);
+        fetch(cok, srow, scol, cv);
+        for (int t0 = 0; t0 < total; t0 += 64) {
+            int nrow = 0, ncol = 0;
+            bool nok = false;
+            if (t0 + 64 < total) nok = locate(t0 + 64, nrow, ncol);
+            fetch(nok, nrow, ncol, nv);
+            if (cok) {
                 const double row_rot = div_sum_w(scol * sa + srow * ca, hw, ihw);
                 const double col_rot = div_sum_w(scol * ca - srow * sa, hw, ihw);
                 const double rb = row_rot + kDescW / 2 - 0.5;
                 const double cb = col_rot + kDescW / 2 - 0.5;
-                const int nx = scol + x, ny = srow + y;
-                const size_t r0 = (size_t)ny * W;
-                const double dx = img[r0 + nx + 1] - img[r0 + nx - 1];
-                const double dy = img[r0 - W + nx] - img[r0 + W + nx];
+                const double dx = cv[0] - cv[1];
+                const double dy = cv[2] - cv[3];
                 const double mag = sqrt(dx * dx + dy * dy);
                 double ang = atan2(dy, dx);
                 ang -= pori;
@@ -924,6 +927,11 @@ __device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevPar
                     }
                 }
             }
+            srow = nrow;
+            scol = ncol;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
+            cok = nok;
         }
     }
     __syncthreads();
@@ -969,12 +977,11 @@ __device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevPar
     }
 }
 
-__global__ __launch_bounds__(256) void k_orient_describe(
+__global__ __launch_bounds__(256) void k_orient(
     const PyrTable* __restrict__ pt, DevParams P, const RawKp* __restrict__ raw,
     const unsigned* __restrict__ raw_begin, const unsigned* __restrict__ n_raw, unsigned cap_raw,
-    sift_kp* __restrict__ recs, double* __restrict__ rec_off0,
-    const unsigned* __restrict__ rec_begin, unsigned* __restrict__ n_rec, unsigned cap_rec,
-    float* __restrict__ desc_f32, unsigned* __restrict__ work, ExportSink ex) {
+    sift_kp* __restrict__ recs, double* __restrict__ rec_off0, unsigned* __restrict__ n_rec,
+    unsigned cap_rec, unsigned* __restrict__ work) {
     __shared__ KpLds S;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1005,18 +1012,32 @@ __global__ __launch_bounds__(256) void k_orient_describe(
         const int side = 2 * radius + 1;
         for (int i = tid; i < 4 * kOriReps * stride; i += 256) S.hist[i] = 0.0;
         __syncthreads();
-        // window rows j (y offset) by chunks of 64 columns i (x offset)
-        const int cpr = (side + 63) >> 6;  // chunks per row
-        const int nchunks = side * cpr;
-        for (int c = wv; c < nchunks; c += 4) {
-            const int jq = c / cpr;
-            const int iq = (c - jq * cpr) * 64 + lane;
-            const int i = iq - radius, j = jq - radius;
-            if (iq < side && !(x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 ||
-                               y + j + 1 >= H)) {
-                const size_t r0 = (size_t)(y + j) * W;
-                const double dx = img[r0 + x + i + 1] - img[r0 + x + i - 1];
-                const double dy = img[r0 - W + x + i] - img[r0 + W + x + i];
+        // the side x side window flattened over the 256 threads (sample s at
+        // offset (i, j) = (s % side, s / side) - radius); the four gradient
+        // loads of a thread's next sample are issued before the current one
+        // is processed
+        const int nsamp = side * side;
+        auto fetch = [&](int s, double* v) -> bool {
+            const int jq = s / side;
+            const int i = s - jq * side - radius, j = jq - radius;
+            if (s >= nsamp || x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H)
+                return false;
+            const size_t r0 = (size_t)(y + j) * W + x + i;
+            v[0] = img[r0 + 1];
+            v[1] = img[r0 - 1];
+            v[2] = img[r0 - W];
+            v[3] = img[r0 + W];
+            return true;
+        };
+        double cv[4], nv[4];
+        bool cok = fetch(tid, cv);
+        for (int s = tid; s < nsamp; s += 256) {
+            const bool nok = fetch(s + 256, nv);
+            if (cok) {
+                const int jq = s / side;
+                const int i = s - jq * side - radius, j = jq - radius;
+                const double dx = cv[0] - cv[1];
+                const double dy = cv[2] - cv[3];
                 const double mag = sqrt(dx * dx + dy * dy);
                 const double ang = atan2(dy, dx);
                 const double wgt = exp(-(i * i + j * j) / denom);
@@ -1024,6 +1045,9 @@ __global__ __launch_bounds__(256) void k_orient_describe(
                 hidx = (hidx < nb) ? hidx : 0;
                 atomicAdd(&rep[hidx], wgt * mag);
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
+            cok = nok;
         }
         __syncthreads();
         for (int b = tid; b < nb; b += 256) {
@@ -1042,7 +1066,11 @@ __global__ __launch_bounds__(256) void k_orient_describe(
                     // h[i+1]: old value, except for i = nb-1 where it is the
                     // already-updated h[0] (and h[0] itself when nb == 1)
                     const double h2 = (i + 1 < nb) ? S.hs[i + 1] : (i == 0 ? h0_old : first_new);
-                    const double v = 0.25 * prev + 0.5 * h1 + 0.25 * h2;
+                    // (0.25 prev + 0.5 h1) + 0.25 h2 in the reference's
+                    // order: the bins are >= 0 and never subnormal, so
+                    // 0.25 * prev is exact and the fma rounds the same sum
+                    // once (one dependent operation less on this lane)
+                    const double v = fma(0.25, prev, 0.5 * h1) + 0.25 * h2;
                     S.hs[i] = v;
                     prev = v;
                     if (i == 0) first_new = v;
@@ -1075,34 +1103,51 @@ __global__ __launch_bounds__(256) void k_orient_describe(
             ry /= 2;
             rs /= 2;
         }
-        for (unsigned p = 0; p < npk; ++p) {
-            const double ori = S.pk[p];
-            if (tid == 0) S.rec = atomicAdd(n_rec, 1u);
-            __syncthreads();
-            const unsigned rec = S.rec;
+        for (unsigned p = tid; p < npk; p += 256) {
+            const unsigned rec = atomicAdd(n_rec, 1u);
             if (rec < cap_rec) {
-                if (tid == 0) {
-                    sift_kp& r = recs[rec];
-                    r.x = rx;
-                    r.y = ry;
-                    r.octave = kp.octave;
-                    r.layer = kp.layer;
-                    r.size = rs;
-                    r.pori = ori;
-                    rec_off0[rec] = kp.off0;
-                }
-                describe(S, pt, P, recs, rec, rx, ry, kp.octave, kp.layer, rs, ori, kp.off0,
-                         desc_f32, ex);
+                sift_kp& r = recs[rec];
+                r.x = rx;
+                r.y = ry;
+                r.octave = kp.octave;
+                r.layer = kp.layer;
+                r.size = rs;
+                r.pori = S.pk[p];
+                rec_off0[rec] = kp.off0;
             }
-            __syncthreads();
         }
+        __syncthreads();
     }
-    // the last workgroup to finish publishes this launch's record range
+}
+
+// Descriptors of records [*rec_begin, *n_rec), one workgroup per record
+// from a work counter; the last workgroup to finish publishes the range.
+__global__ __launch_bounds__(256, 3) void k_descriptor(const PyrTable* __restrict__ pt, DevParams P,
+                                                    sift_kp* __restrict__ recs,
+                                                    const double* __restrict__ rec_off0,
+                                                    const unsigned* __restrict__ rec_begin,
+                                                    const unsigned* __restrict__ n_rec,
+                                                    unsigned cap_rec, float* __restrict__ desc_f32,
+                                                    unsigned* __restrict__ work, ExportSink ex) {
+    __shared__ KpLds S;
+    const int tid = threadIdx.x;
+    const unsigned n = min(*n_rec, cap_rec);
+    const unsigned k0 = min(*rec_begin, n);
+    for (;;) {
+        if (tid == 0) S.k = k0 + atomicAdd(work, 1u);
+        __syncthreads();
+        const unsigned k = S.k;
+        if (k >= n) break;
+        const double* hdr = reinterpret_cast<const double*>(&recs[k]);
+        describe(S, pt, P, recs, k, hdr[0], hdr[1], reinterpret_cast<const int*>(hdr)[4],
+                 reinterpret_cast<const int*>(hdr)[5], hdr[3], hdr[4], rec_off0[k], desc_f32, ex);
+        __syncthreads();
+    }
     if (ex.cnt && tid == 0) {
         __threadfence();
         if (atomicAdd(work + 1, 1u) == gridDim.x - 1) {
-            ex.cnt[0] = *rec_begin;
-            ex.cnt[1] = atomicAdd(n_rec, 0u);
+            ex.cnt[0] = k0;
+            ex.cnt[1] = n;
         }
     }
 }
@@ -1240,15 +1285,14 @@ hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double
 
 hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
                                 int thr, sift_extremum* out, unsigned* counter, unsigned cap,
-                                const DevParams& P, RawKp* raw, unsigned* n_raw,
-                                unsigned cap_raw, hipStream_t s) {
+                                hipStream_t s) {
     const int blocks = eg.first_tile[eg.n];
     if (blocks == 0) return hipSuccess;
     switch (n_gauss) {
 #define SIFT_EXT_CASE(NL)                                                                 \
     case NL:                                                                              \
         hipLaunchKernelGGL((k_extrema_tiles<NL>), dim3(blocks), dim3(256), 0, s, d_pt, eg, \
-                           thr, out, counter, cap, P, raw, n_raw, cap_raw);               \
+                           thr, out, counter, cap);                                       \
         return hipGetLastError();
         SIFT_EXT_CASE(4)
         SIFT_EXT_CASE(5)
@@ -1295,18 +1339,26 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
     return hipGetLastError();
 }
 
-hipError_t launch_orient_describe(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
-                                  const unsigned* raw_begin, const unsigned* n_raw,
-                                  unsigned cap_raw, sift_kp* recs, double* rec_off0,
-                                  const unsigned* rec_begin, unsigned* n_rec, unsigned cap_rec,
-                                  float* desc_f32, unsigned* work, const ExportSink& ex,
-                                  hipStream_t s) {
-    // persistent: 4 workgroups per CU pull keypoints from the work counter
-    unsigned blocks = 1024;
+hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
+                         const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
+                         sift_kp* recs, double* rec_off0, unsigned* n_rec, unsigned cap_rec,
+                         unsigned* work, unsigned wgs, hipStream_t s) {
+    unsigned blocks = wgs;  // persistent: workgroups pull keypoints
     if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
-    hipLaunchKernelGGL(k_orient_describe, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin,
-                       n_raw, cap_raw, recs, rec_off0, rec_begin, n_rec, cap_rec, desc_f32, work,
-                       ex);
+    hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin, n_raw,
+                       cap_raw, recs, rec_off0, n_rec, cap_rec, work);
+    return hipGetLastError();
+}
+
+hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
+                             const double* rec_off0, const unsigned* rec_begin,
+                             const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
+                             unsigned* work, const ExportSink& ex, unsigned wgs,
+                             hipStream_t s) {
+    unsigned blocks = wgs;  // persistent: workgroups pull records
+    if (blocks > cap_rec) blocks = cap_rec > 0 ? cap_rec : 1;
+    hipLaunchKernelGGL(k_descriptor, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_off0,
+                       rec_begin, n_rec, cap_rec, desc_f32, work, ex);
     return hipGetLastError();
 }
 

@@ -68,4 +68,4 @@ def test_null_args_are_rejected_without_gpu():
 def test_kernels_are_gfx950_code_objects():
     blob = open(LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    assert b"k_blur" in blob and b"k_orient_describe" in blob
+    assert b"k_blur" in blob and b"k_orient" in blob and b"k_descriptor" in blob
