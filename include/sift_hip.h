@@ -125,6 +125,32 @@ int sift_hip_detect_device(sift_ctx* ctx, const double* d_hwc, int w, int h,
 void sift_hip_free(void* p);
 const char* sift_hip_strerror(int status);
 
+/* ---- matcher -------------------------------------------------------------- */
+/*
+ * Brute-force 2-NN ratio-test matcher (reference match_keypoints,
+ * src/sift.cpp:783-815, with euclid_dist :688-695): for each record i1 of
+ * kps1, the nearest (i2) and second-nearest records of kps2 by Euclidean
+ * distance over the 128 descriptor bytes; a match when
+ * best < ratio_threshold * second (second = DBL_MAX when n2 == 1). Matches
+ * come in increasing i1 order, as the reference's vector; ties resolve as the
+ * reference's scan (lowest i2 wins). n2 == 0 gives no matches (the reference
+ * is undefined there for ratio > 1). *out is allocated by the library
+ * (release with sift_hip_free; NULL when *n_out == 0).
+ */
+typedef struct sift_match_pair {
+    uint32_t i1;      /* index into kps1 (KeypointMatch::kp1) */
+    uint32_t i2;      /* index into kps2 (KeypointMatch::kp2) */
+    double distance;  /* KeypointMatch::distance */
+} sift_match_pair;
+
+int sift_hip_match(sift_ctx* ctx, const sift_kp* kps1, size_t n1, const sift_kp* kps2,
+                   size_t n2, double ratio_threshold, sift_match_pair** out, size_t* n_out);
+
+/* Same with both record arrays resident on the context's device. */
+int sift_hip_match_device(sift_ctx* ctx, const sift_kp* d_kps1, size_t n1,
+                          const sift_kp* d_kps2, size_t n2, double ratio_threshold,
+                          sift_match_pair** out, size_t* n_out);
+
 /* ---- introspection of the last detect (tests, bench, multi-GPU) -------- */
 
 /* Pipeline counts of the last detect: extrema candidates, refined

@@ -17,6 +17,7 @@
 //
 // usage: ref_harness <input> <out_prefix> [intervals=3] [double=1]
 //                    [max_octaves=0] [dump_pyramid=0]
+//        ref_harness --match <kps1.bin> <kps2.bin> <ratio> <out.bin>
 //   <input> is an image file (stb decode, image_io.cpp:20-35) or a raw file
 //   "SIFTRAW1" + int32 w,h,c + w*h*c little-endian doubles.
 #include <cstdio>
@@ -65,7 +66,42 @@ struct ExtRec {
 
 }  // namespace
 
+// --match <kps1.bin> <kps2.bin> <ratio> <out.bin>: the reference
+// match_keypoints (sift.cpp:783-815) on two raw Keypoint arrays; writes one
+// (int32 i1, int32 i2, double distance) triple per match, the indices
+// recovered by byte comparison of the copies KeypointMatch holds.
+int match_mode(char** argv) {
+    auto load = [](const char* path) {
+        std::ifstream f(path, std::ios::binary | std::ios::ate);
+        const size_t bytes = (size_t)f.tellg();
+        std::vector<Keypoint> v(bytes / sizeof(Keypoint));
+        f.seekg(0);
+        f.read(reinterpret_cast<char*>(v.data()), v.size() * sizeof(Keypoint));
+        return v;
+    };
+    const std::vector<Keypoint> a = load(argv[2]), b = load(argv[3]);
+    const double ratio = std::atof(argv[4]);
+    std::streambuf* saved = std::cout.rdbuf(nullptr);
+    const std::vector<KeypointMatch> m = match_keypoints(a, b, ratio);
+    std::cout.rdbuf(saved);
+    std::ofstream f(argv[5], std::ios::binary);
+    size_t i1 = 0;
+    for (const KeypointMatch& k : m) {
+        while (i1 < a.size() && std::memcmp(&a[i1], &k.kp1, sizeof(Keypoint)) != 0) ++i1;
+        size_t i2 = 0;
+        while (i2 < b.size() && std::memcmp(&b[i2], &k.kp2, sizeof(Keypoint)) != 0) ++i2;
+        if (i1 == a.size() || i2 == b.size()) return 3;
+        const int32_t idx[2] = {(int32_t)i1, (int32_t)i2};
+        f.write(reinterpret_cast<const char*>(idx), sizeof idx);
+        f.write(reinterpret_cast<const char*>(&k.distance), sizeof(double));
+        ++i1;
+    }
+    std::printf("match: %zu x %zu -> %zu\n", a.size(), b.size(), m.size());
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 6 && std::strcmp(argv[1], "--match") == 0) return match_mode(argv);
     if (argc < 3) {
         std::fprintf(stderr, "usage: %s <input> <out_prefix> [intervals] [double] [max_octaves] [dump_pyr]\n", argv[0]);
         return 2;

@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 #include <vector>
 
 #include "../include/sift_hip.h"
@@ -603,6 +604,41 @@ size_t sift_cpu_final(void* run, const sift_kp** out, const float** desc_f32) {
 void sift_cpu_times(void* run, double* t8) {
     Run* R = static_cast<Run*>(run);
     for (int i = 0; i < 8; ++i) t8[i] = R->t[i];
+}
+
+// match_keypoints (reference sift.cpp:783-815) with euclid_dist
+// (sift.cpp:688-695), same scan and update order: out_j[i] = index into k2 of
+// the match of k1[i], or -1; out_d[i] = its best distance. Returns the match
+// count. n2 == 0 gives no matches (the reference would read keypoints2[0]
+// there when ratio > 1).
+size_t sift_cpu_match(const sift_kp* k1, size_t n1, const sift_kp* k2, size_t n2, double ratio,
+                      int* out_j, double* out_d) {
+    size_t m = 0;
+    for (size_t i = 0; i < n1; ++i) {
+        double best = std::numeric_limits<double>::max();
+        double second = std::numeric_limits<double>::max();
+        size_t best_j = 0;
+        for (size_t j = 0; j < n2; ++j) {
+            double sum = 0.0;
+            for (int t = 0; t < 128; ++t) {
+                const int diff = (int)k1[i].desc[t] - (int)k2[j].desc[t];
+                sum += diff * diff;
+            }
+            const double dist = std::sqrt(sum);
+            if (dist < best) {
+                second = best;
+                best = dist;
+                best_j = j;
+            } else if (dist < second) {
+                second = dist;
+            }
+        }
+        const bool ok = n2 > 0 && best < ratio * second;
+        out_j[i] = ok ? (int)best_j : -1;
+        out_d[i] = best;
+        m += ok;
+    }
+    return m;
 }
 
 // Same defaults as the product library (reference sift.hh:65-71); defined

@@ -94,33 +94,25 @@ std::vector<Keypoint> detect_keypoints_and_descriptors(
     return out;
 }
 
-// 2-NN ratio test over integer L2 distances (reference sift.cpp:688-695,
-// 783-815): strict '<' updates, so the first best index wins ties.
+// 2-NN ratio test (reference sift.cpp:688-695, 783-815) on the GPU matcher
+// (sift_hip_match, csrc/sift_match.hip): same matches, same order, same
+// distances; KeypointMatch copies the records as the reference does.
 std::vector<KeypointMatch> match_keypoints(const std::vector<Keypoint>& keypoints1,
                                            const std::vector<Keypoint>& keypoints2,
                                            double ratio_threshold) {
     std::vector<KeypointMatch> matches;
-    for (const Keypoint& a : keypoints1) {
-        double best = std::numeric_limits<double>::max();
-        double second = std::numeric_limits<double>::max();
-        size_t best_j = 0;
-        for (size_t j = 0; j < keypoints2.size(); ++j) {
-            double ss = 0.0;
-            for (int i = 0; i < 128; ++i) {
-                const int d = (int)a.desc[i] - (int)keypoints2[j].desc[i];
-                ss += d * d;
-            }
-            const double dist = std::sqrt(ss);
-            if (dist < best) {
-                second = best;
-                best = dist;
-                best_j = j;
-            } else if (dist < second) {
-                second = dist;
-            }
-        }
-        if (best < ratio_threshold * second) matches.emplace_back(a, keypoints2[best_j], best);
-    }
+    sift_match_pair* pairs = nullptr;
+    size_t n = 0;
+    const int st = sift_hip_match(
+        thread_context(), reinterpret_cast<const sift_kp*>(keypoints1.data()), keypoints1.size(),
+        reinterpret_cast<const sift_kp*>(keypoints2.data()), keypoints2.size(), ratio_threshold,
+        &pairs, &n);
+    if (st != SIFT_OK)
+        throw std::runtime_error(std::string("match_keypoints: ") + sift_hip_strerror(st));
+    std::unique_ptr<sift_match_pair, void (*)(void*)> guard(pairs, sift_hip_free);
+    matches.reserve(n);
+    for (size_t k = 0; k < n; ++k)
+        matches.emplace_back(keypoints1[pairs[k].i1], keypoints2[pairs[k].i2], pairs[k].distance);
     return matches;
 }
 

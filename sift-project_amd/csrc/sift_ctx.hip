@@ -154,6 +154,13 @@ struct sift_ctx {
     std::vector<hipEvent_t> chain_ev;
     std::vector<unsigned> run_start;
 
+    // matcher: one device arena (inputs, shifted rows, norms, results) and
+    // pinned result staging
+    unsigned char* d_mbuf = nullptr;
+    size_t mbuf_cap = 0;
+    Pinned<int> h_mj;
+    Pinned<double> h_md;
+
     // host staging (pinned)
     Pinned<sift_kp> h_ori;
     Pinned<double> h_off0;
@@ -679,7 +686,8 @@ int sift_hip_destroy(sift_ctx* ctx) {
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
     void* bufs[] = {ctx->d_in, ctx->d_pyr, ctx->d_tmp, ctx->d_cand, ctx->d_raw,
-                    ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_stage};
+                    ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_stage,
+                    ctx->d_mbuf};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->h_ctr) (void)hipHostFree(ctx->h_ctr);
@@ -691,6 +699,8 @@ int sift_hip_destroy(sift_ctx* ctx) {
     for (hipEvent_t e : ctx->chain_ev) (void)hipEventDestroy(e);
     ctx->h_off0.release();
     ctx->h_df32.release();
+    ctx->h_mj.release();
+    ctx->h_md.release();
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -730,6 +740,96 @@ int sift_hip_detect_device(sift_ctx* ctx, const double* d_hwc, int w, int h, int
         p = &def;
     }
     return detect_impl(ctx, d_hwc, w, h, c, p, out_kps, out_n, out_desc_f32);
+}
+
+namespace {
+
+// sift_hip_match / sift_hip_match_device (sift_match.hip does the work): both
+// record lists -> shifted rows + norms, one 2-NN launch, per-query results
+// back to the host, compacted in query order.
+static int match_impl(sift_ctx* ctx, const sift_kp* k1, size_t n1, const sift_kp* k2, size_t n2,
+               bool on_device, double ratio, sift_match_pair** out, size_t* n_out) {
+    if (!ctx || !out || !n_out) return SIFT_ERR_ARG;
+    *out = nullptr;
+    *n_out = 0;
+    if ((n1 && !k1) || (n2 && !k2)) return SIFT_ERR_ARG;
+    if (n1 > (1u << 28) || n2 > (1u << 28)) return SIFT_ERR_ARG;
+    if (n1 == 0 || n2 == 0) return SIFT_OK;
+    SIFT_HIP_TRY(hipSetDevice(ctx->device));
+    const size_t n1p = (n1 + 31) & ~(size_t)31, n2p = (n2 + 31) & ~(size_t)31;
+    auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_k1 = 0;
+    const size_t o_k2 = o_k1 + (on_device ? 0 : up(n1 * sizeof(sift_kp)));
+    const size_t o_r1 = o_k2 + (on_device ? 0 : up(n2 * sizeof(sift_kp)));
+    const size_t o_r2 = o_r1 + up(n1p * 128);
+    const size_t o_q1 = o_r2 + up(n2p * 128);
+    const size_t o_q2 = o_q1 + up(n1p * sizeof(int));
+    const size_t o_j = o_q2 + up(n2p * sizeof(int));
+    const size_t o_d = o_j + up(n1 * sizeof(int));
+    const size_t need = o_d + up(n1 * sizeof(double));
+    if (ctx->mbuf_cap < need) {
+        if (ctx->d_mbuf) (void)hipFree(ctx->d_mbuf);
+        ctx->d_mbuf = nullptr;
+        ctx->mbuf_cap = 0;
+        if (hipMalloc(&ctx->d_mbuf, need) != hipSuccess) return SIFT_ERR_NOMEM;
+        ctx->mbuf_cap = need;
+    }
+    int st;
+    if ((st = ctx->h_mj.ensure(n1)) != SIFT_OK || (st = ctx->h_md.ensure(n1)) != SIFT_OK)
+        return st;
+    unsigned char* b = ctx->d_mbuf;
+    hipStream_t s = ctx->stream;
+    const sift_kp* d1 = k1;
+    const sift_kp* d2 = k2;
+    if (!on_device) {
+        SIFT_HIP_TRY(hipMemcpyAsync(b + o_k1, k1, n1 * sizeof(sift_kp), hipMemcpyHostToDevice, s));
+        SIFT_HIP_TRY(hipMemcpyAsync(b + o_k2, k2, n2 * sizeof(sift_kp), hipMemcpyHostToDevice, s));
+        d1 = reinterpret_cast<const sift_kp*>(b + o_k1);
+        d2 = reinterpret_cast<const sift_kp*>(b + o_k2);
+    }
+    uint8_t* r1 = b + o_r1;
+    uint8_t* r2 = b + o_r2;
+    int* q1 = reinterpret_cast<int*>(b + o_q1);
+    int* q2 = reinterpret_cast<int*>(b + o_q2);
+    int* dj = reinterpret_cast<int*>(b + o_j);
+    double* dd = reinterpret_cast<double*>(b + o_d);
+    SIFT_HIP_TRY(launch_match_prep(d1, (unsigned)n1, (unsigned)n1p, r1, q1, s));
+    SIFT_HIP_TRY(launch_match_prep(d2, (unsigned)n2, (unsigned)n2p, r2, q2, s));
+    SIFT_HIP_TRY(launch_match2nn(r1, q1, (unsigned)n1, (unsigned)n1p, r2, q2, (unsigned)n2p,
+                                 ratio, dj, dd, s));
+    SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_mj.p, dj, n1 * sizeof(int), hipMemcpyDeviceToHost, s));
+    SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_md.p, dd, n1 * sizeof(double), hipMemcpyDeviceToHost, s));
+    SIFT_HIP_TRY(hipStreamSynchronize(s));
+    size_t m = 0;
+    for (size_t i = 0; i < n1; ++i) m += ctx->h_mj.p[i] >= 0;
+    if (m == 0) return SIFT_OK;
+    sift_match_pair* res = static_cast<sift_match_pair*>(std::malloc(m * sizeof(sift_match_pair)));
+    if (!res) return SIFT_ERR_NOMEM;
+    size_t k = 0;
+    for (size_t i = 0; i < n1; ++i) {
+        const int j = ctx->h_mj.p[i];
+        if (j < 0) continue;
+        res[k].i1 = (uint32_t)i;
+        res[k].i2 = (uint32_t)j;
+        res[k].distance = ctx->h_md.p[i];
+        ++k;
+    }
+    *out = res;
+    *n_out = m;
+    return SIFT_OK;
+}
+
+}  // namespace
+
+int sift_hip_match(sift_ctx* ctx, const sift_kp* kps1, size_t n1, const sift_kp* kps2,
+                   size_t n2, double ratio_threshold, sift_match_pair** out, size_t* n_out) {
+    return match_impl(ctx, kps1, n1, kps2, n2, false, ratio_threshold, out, n_out);
+}
+
+int sift_hip_match_device(sift_ctx* ctx, const sift_kp* d_kps1, size_t n1,
+                          const sift_kp* d_kps2, size_t n2, double ratio_threshold,
+                          sift_match_pair** out, size_t* n_out) {
+    return match_impl(ctx, d_kps1, n1, d_kps2, n2, true, ratio_threshold, out, n_out);
 }
 
 void sift_hip_free(void* p) { std::free(p); }

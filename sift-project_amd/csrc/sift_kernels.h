@@ -57,4 +57,14 @@ hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* 
                              unsigned* work, const ExportSink& ex, unsigned wgs,
                              hipStream_t s);
 
+// Matcher (sift_match.hip): records -> shifted descriptor rows + norms
+// (n_pad a multiple of 32, rows [n, n_pad) padding), then the 2-NN ratio test
+// of queries [0, n1) against the n2_pad reference rows: out_j[i] = index of
+// the match or -1, out_d[i] = best distance.
+hipError_t launch_match_prep(const sift_kp* d_kps, unsigned n, unsigned n_pad, uint8_t* rows,
+                             int* q, hipStream_t s);
+hipError_t launch_match2nn(const uint8_t* qrows, const int* qq, unsigned n1, unsigned n1_pad,
+                           const uint8_t* rrows, const int* rq, unsigned n2_pad, double ratio,
+                           int* out_j, double* out_d, hipStream_t s);
+
 }  // namespace sift_amd

@@ -36,6 +36,10 @@ assert KP_DTYPE.itemsize == 168
 
 EXT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("z", "<i4"), ("octave", "<i4")])
 
+# sift_match_pair (include/sift_hip.h): KeypointMatch (reference sift.hh:55-63)
+# as indices into the two keypoint lists plus the distance
+MATCH_DTYPE = np.dtype([("i1", "<u4"), ("i2", "<u4"), ("distance", "<f8")])
+
 ERRORS = {
     0: "ok",
     -1: "invalid argument",
@@ -57,6 +61,8 @@ EXPORTS = (
     "sift_hip_detect_device",
     "sift_hip_free",
     "sift_hip_strerror",
+    "sift_hip_match",
+    "sift_hip_match_device",
     "sift_hip_last_counts",
     "sift_hip_copy_level",
     "sift_hip_copy_extrema",
@@ -151,6 +157,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sift_hip_free.restype = None
     lib.sift_hip_strerror.argtypes = [i]
     lib.sift_hip_strerror.restype = ctypes.c_char_p
+    match_args = [vp, vp, sz, vp, sz, ctypes.c_double, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+    lib.sift_hip_match.argtypes = match_args
+    lib.sift_hip_match_device.argtypes = match_args
     lib.sift_hip_last_counts.argtypes = [vp, ctypes.POINTER(CCounts)]
     lib.sift_hip_copy_level.argtypes = [vp, i, i, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
     lib.sift_hip_copy_extrema.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
@@ -250,6 +259,33 @@ class Context:
                                                ctypes.byref(df_ptr) if desc_f32 else None))
         return self._finish(kp_ptr, n, df_ptr, desc_f32)
 
+    def _match_result(self, out, n):
+        try:
+            return np.frombuffer(ctypes.string_at(out.value, n.value * 16), dtype=MATCH_DTYPE) \
+                .copy() if n.value else np.zeros(0, dtype=MATCH_DTYPE)
+        finally:
+            self.lib.sift_hip_free(out)
+
+    def match(self, kps1: np.ndarray, kps2: np.ndarray, ratio_threshold: float = 0.75):
+        """match_keypoints (reference sift.cpp:783-815) on the GPU: structured
+        array (i1, i2, distance) in increasing i1, indices into kps1 / kps2."""
+        a = np.ascontiguousarray(kps1, dtype=KP_DTYPE)
+        b = np.ascontiguousarray(kps2, dtype=KP_DTYPE)
+        out, n = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(self.lib.sift_hip_match(self._ctx, a.ctypes.data if len(a) else None, len(a),
+                                       b.ctypes.data if len(b) else None, len(b),
+                                       ratio_threshold, ctypes.byref(out), ctypes.byref(n)))
+        return self._match_result(out, n)
+
+    def match_device(self, d_kps1: int, n1: int, d_kps2: int, n2: int,
+                     ratio_threshold: float = 0.75):
+        """Same with both record arrays already in HBM (device pointers)."""
+        out, n = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(self.lib.sift_hip_match_device(self._ctx, ctypes.c_void_p(d_kps1), n1,
+                                              ctypes.c_void_p(d_kps2), n2, ratio_threshold,
+                                              ctypes.byref(out), ctypes.byref(n)))
+        return self._match_result(out, n)
+
     def counts(self) -> dict:
         c = CCounts()
         _check(self.lib.sift_hip_last_counts(self._ctx, ctypes.byref(c)))
@@ -316,6 +352,12 @@ def detect_keypoints_and_descriptors(img: np.ndarray, double_image_size: bool = 
                    eigen_ratio, num_bins, peak_ratio, ori_sigma_factor, desc_scale_factor)
     kps, _ = ctx.detect(img, p)
     return kps
+
+
+def match_keypoints(keypoints1: np.ndarray, keypoints2: np.ndarray,
+                    ratio_threshold: float = 0.75, device: int = 0):
+    """Functional mirror of match_keypoints (reference sift.hh:73-75)."""
+    return _default_context(device).match(keypoints1, keypoints2, ratio_threshold)
 
 
 _contexts: dict = {}

@@ -19,7 +19,7 @@ Each case becomes tests/golden/<name>.npz (allow_pickle=False) holding:
   pyr_sha256       sha256 of every Gaussian level, octave-major (small cases)
   input_u8         the decoded input (image1 only)
 
-usage: python tests/golden/make_goldens.py [--big]
+usage: python tests/golden/make_goldens.py [--big] | --match
 """
 from __future__ import annotations
 
@@ -41,6 +41,7 @@ from sift_hip import KP_DTYPE, synth_image  # noqa: E402
 HARNESS_CF = os.path.join(ROOT, "oracle", "_ref", "ref_harness_cf")
 HARNESS_ASIS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 IMAGE1 = "/root/reference/stitching/image1.jpg"
+IMAGE2 = "/root/reference/stitching/image2.jpg"
 
 # name: (w, h, c, nblobs-or-None, smax, seed, intervals, double, max_octaves,
 #        kind) where kind: "small" (full dump + as-is cross-check),
@@ -171,6 +172,62 @@ def make_case(name, spec, tmp):
           f"final={meta['final']} ref_total={meta['ref_time_s'].get('total', 0):.2f}s")
 
 
+def ref_match(k1, k2, ratio, tmp):
+    """The reference match_keypoints (sift.cpp:783-815) via `ref_harness --match`."""
+    a, b, o = (os.path.join(tmp, n) for n in ("m1.bin", "m2.bin", "mo.bin"))
+    k1.tofile(a)
+    k2.tofile(b)
+    subprocess.run([HARNESS_ASIS, "--match", a, b, repr(float(ratio)), o], check=True,
+                   stdout=subprocess.DEVNULL)
+    return np.fromfile(o, dtype=MATCH_DTYPE)
+
+
+MATCH_DTYPE = np.dtype([("i1", "<i4"), ("i2", "<i4"), ("distance", "<f8")])
+
+
+def records_from_desc(desc):
+    """Keypoint records carrying only descriptors (x = index keeps them distinct)."""
+    k = np.zeros(len(desc), dtype=KP_DTYPE)
+    k["x"] = np.arange(len(desc))
+    k["desc"] = desc
+    return k
+
+
+def make_match(tmp):
+    """tests/golden/match_cases.npz: the reference matcher on
+      image1_image2  final keypoints of stitching/image1.jpg vs image2.jpg
+                     (main.cpp:15-17, ratio 0.75 = sift.hh default)
+      ties_*         tie-heavy descriptors (bytes in {0,1,2}, duplicated rows)
+                     at ratios 0.75, 1.0, 1.5
+      single_ref     n2 == 1 (second distance = DBL_MAX)
+    Each case stores desc1, desc2 (u8 [n,128]), ratio and matches (i1, i2, d)."""
+    out = {}
+    finals = []
+    for img in (IMAGE1, IMAGE2):
+        prefix = os.path.join(tmp, os.path.basename(img) + "_m")
+        run_harness(HARNESS_CF, img, prefix, 3, 1, 0, False)
+        finals.append(np.fromfile(prefix + ".final.bin", dtype=KP_DTYPE))
+    cases = {"image1_image2": (finals[0]["desc"], finals[1]["desc"], 0.75)}
+    rng = np.random.default_rng(5)
+    d1 = rng.integers(0, 3, size=(300, 128), dtype=np.uint8)
+    d2 = rng.integers(0, 3, size=(257, 128), dtype=np.uint8)
+    d2[100:140] = d2[60:100]        # exact duplicate references
+    d1[:40] = d2[60:100]            # queries equal to duplicated references
+    d1[40:60] = d2[0:20]            # queries equal to unique references
+    for r in (0.75, 1.0, 1.5):
+        cases[f"ties_{r}"] = (d1, d2, r)
+    cases["single_ref"] = (d1[:37], d2[5:6], 0.75)
+    for name, (a, b, r) in cases.items():
+        m = ref_match(records_from_desc(a), records_from_desc(b), r, tmp)
+        out[name + "__desc1"] = a
+        out[name + "__desc2"] = b
+        out[name + "__ratio"] = np.array(r)
+        out[name + "__matches"] = m
+        print(f"match {name}: {len(a)} x {len(b)} ratio {r} -> {len(m)} matches")
+    out["names"] = np.array(list(cases))
+    np.savez_compressed(os.path.join(HERE, "match_cases.npz"), **out)
+
+
 def main():
     for exe in (HARNESS_CF, HARNESS_ASIS):
         if not os.path.exists(exe):
@@ -179,6 +236,10 @@ def main():
     if "--big" in sys.argv:
         cases.update(BIG_CASES)
     only = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--match" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            make_match(tmp)
+        return
     with tempfile.TemporaryDirectory() as tmp:
         for name, spec in cases.items():
             if only and name not in only:

@@ -59,6 +59,8 @@ class Golden:
 def all_goldens(kinds=("small", "medium", "big")):
     out = []
     for p in sorted(glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))):
+        if os.path.basename(p) == "match_cases.npz":  # matcher goldens (test_match.py)
+            continue
         g = Golden(p)
         if g.kind in kinds:
             out.append(g)
