@@ -72,6 +72,41 @@ def cpu_baseline(img: np.ndarray, seconds: float) -> dict:
     }
 
 
+def matcher_bench(ctx, dev, kps_a, W, H, params, cpu_seconds: float) -> dict:
+    """the GPU matcher (match_keypoints, sift.cpp:783-815) on
+    the bench image's keypoints against those of a second synthetic image
+    (seed 43), both record arrays resident in HBM; wall time per call incl.
+    the result download and compaction. CPU baseline: the oracle matcher on a
+    bounded sample of queries against all references, 1 core."""
+    kps_b, _ = ctx.detect(synth_image(W, H, 1, seed=43), params)
+    da = torch.from_numpy(kps_a.view(np.uint8).copy()).to(dev)
+    db = torch.from_numpy(kps_b.view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        m = ctx.match_device(da.data_ptr(), len(kps_a), db.data_ptr(), len(kps_b), 0.75)
+    reps = 50
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        m = ctx.match_device(da.data_ptr(), len(kps_a), db.data_ptr(), len(kps_b), 0.75)
+    dt = (time.perf_counter() - t0) / reps
+    pairs = float(len(kps_a)) * len(kps_b)
+    out = {"n1": len(kps_a), "n2": len(kps_b), "ratio": 0.75, "matches": len(m),
+           "ms_per_match": dt * 1e3, "pairs_per_s": pairs / dt}
+    if cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_bind import oracle_match
+        nq, t = 0, 0.0
+        t0 = time.perf_counter()
+        while t < cpu_seconds * 0.2:
+            oracle_match(kps_a[nq % len(kps_a):nq % len(kps_a) + 64], kps_b, 0.75)
+            nq += 64
+            t = time.perf_counter() - t0
+        out["cpu_baseline"] = {"pairs_per_s": nq * len(kps_b) / t, "cores": 1, "kind": "port",
+                               "sample": f"{nq} queries x {len(kps_b)} references, "
+                                         f"oracle/sift_cpu.cpp sift_cpu_match, {t:.1f} s"}
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,6 +117,8 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-matcher", action="store_true",
+                    help="skip the matcher measurement (SURVEY §8f row 1)")
     ap.add_argument("--no-events", action="store_true",
                     help="skip the per-launch HIP events of the pyramid roofline")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "blur_traffic.json"),
@@ -199,6 +236,10 @@ def main() -> int:
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(host_imgs[0], args.cpu_seconds)
+        if world == 1 and not args.no_matcher:
+            kps_a, _ = ctx.detect_device(dev_imgs[0].data_ptr(), W, H, 1, params)
+            out["matcher"] = matcher_bench(ctx, dev, kps_a, W, H, params,
+                                           0.0 if args.no_cpu_baseline else args.cpu_seconds)
         print(json.dumps(out), flush=True)
 
     ctx.close()

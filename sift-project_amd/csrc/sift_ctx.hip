@@ -104,6 +104,7 @@ struct sift_ctx {
     hipStream_t stream = nullptr;   // A: pyramid
     hipStream_t stream2 = nullptr;  // B: odd octaves of the pyramid
     hipStream_t stream3 = nullptr;  // C: extrema, refine, orientation, descriptor
+    hipStream_t stream4 = nullptr;  // D (optional): extrema, overlapping C's chains
     // persistent workgroups of orientation / descriptor: 768 = what fits at
     // once (3 per CU at the descriptor's 168 VGPRs); measured best of
     // 512/768/1024 (CU-masking stream C was measured slower)
@@ -310,7 +311,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     // exist, the extrema then refine -> orientation -> descriptor. The
     // keypoint work of octave 0 overlaps the pyramid of the smaller octaves,
     // which is latency-bound and leaves most of the chip idle.
-    hipStream_t sA = ctx->stream, sB = ctx->stream2, sC = ctx->stream3;
+    hipStream_t sA = ctx->stream, sB = ctx->stream2, sC = ctx->stream3, sD = ctx->stream4;
     int ev_i = 0;
 
     SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sA));
@@ -365,16 +366,16 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         }
     const unsigned* zeros = ctx->d_ctr + kCtrZeros;
     auto snap = [&](int g) { return ctx->d_ctr + kCtrSnap + 4 * g; };
-    auto launch_extrema_range = [&](int o_begin, int o_end) -> int {
+    auto launch_extrema_range = [&](int o_begin, int o_end, hipStream_t sx) -> int {
         if (tiles) {
             const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
             SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
-                                              ctx->d_ctr + 0, ctx->cap_cand, sC));
+                                              ctx->d_ctr + 0, ctx->cap_cand, sx));
         } else {
             for (int o = o_begin; o < o_end; ++o)
                 SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
                                                 p->window_size, dp.threshold, ctx->d_cand,
-                                                ctx->d_ctr + 0, ctx->cap_cand, sC));
+                                                ctx->d_ctr + 0, ctx->cap_cand, sx));
         }
         return SIFT_OK;
     };
@@ -392,8 +393,12 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     // `begin` (a counter snapshot taken right after the extrema) holds this
     // batch's candidate end and its raw / record begins; candidates start at
     // cand_begin (the previous batch's snapshot). The re-run passes nullptr.
+    // With stream D the extrema of batch g run there as soon as their levels
+    // exist, overlapping the keypoint chain of batch g-1 on C: D snapshots the
+    // candidate end, C (after its previous chain) the raw / record begins.
     auto run_chain = [&](int o_begin, int o_end, const unsigned* cand_begin,
                          unsigned* begin) -> int {
+        const bool split = sD && begin;
         const int ci = n_chains++;
         unsigned* work = ctx->d_ctr + kCtrWork + 4 * ci;
         while ((int)ctx->chain_ev.size() <= ci) {
@@ -404,12 +409,22 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         }
         const ExportSink ex{ctx->exp_rec.d, ctx->exp_off0.d, ctx->exp_cnt.d + 2 * ci,
                             (unsigned)ctx->exp_rec.cap};
-        int st2 = launch_extrema_range(o_begin, o_end);
+        int st2 = launch_extrema_range(o_begin, o_end, split ? sD : sC);
         if (st2 != SIFT_OK) return st2;
-        if (begin) SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
+        if (split) {
+            SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sD, 0, 1));
+            hipEvent_t ext_done = sync_event(ctx, ev_i++);
+            if (!ext_done) return SIFT_ERR_HIP;
+            SIFT_HIP_TRY(hipEventRecord(ext_done, sD));
+            SIFT_HIP_TRY(hipStreamWaitEvent(sC, ext_done, 0));
+            SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC, 1, 3));
+        } else if (begin) {
+            SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
+        }
         const unsigned* b = begin ? begin : zeros;
-        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin, ctx->d_ctr + 0,
-                                   ctx->cap_cand, ctx->d_raw, ctx->d_ctr + 1, ctx->cap_raw, sC));
+        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin,
+                                   begin ? begin : ctx->d_ctr + 0, ctx->cap_cand, ctx->d_raw,
+                                   ctx->d_ctr + 1, ctx->cap_raw, sC));
         SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, b + 1, ctx->d_ctr + 1, ctx->cap_raw,
                                    ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2, ctx->cap_ori, work,
                                    ctx->kp_wgs, sC));
@@ -428,7 +443,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             hipEvent_t pyr_done = sync_event(ctx, ev_i++);
             if (!pyr_done) return SIFT_ERR_HIP;
             SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
-            SIFT_HIP_TRY(hipStreamWaitEvent(sC, pyr_done, 0));
+            SIFT_HIP_TRY(hipStreamWaitEvent(sD ? sD : sC, pyr_done, 0));
         }
         return run_chain(o_begin, o_end, gb == 0 ? zeros : snap(gb - 1), snap(gb));
     };
@@ -661,6 +676,13 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::atoi(e);
     if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
     if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) ctx->batch_px_log2 = std::atoi(e);
+    const char* ext_stream = std::getenv("SIFT_EXT_STREAM");
+    if (ext_stream && std::atoi(ext_stream) > 0 &&
+        hipStreamCreateWithPriority(&ctx->stream4, hipStreamNonBlocking,
+                                    std::atoi(ext_stream) > 1 ? prio_hi : prio_lo) != hipSuccess) {
+        sift_hip_destroy(ctx);
+        return SIFT_ERR_HIP;
+    }
     if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 20;
     if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
@@ -685,6 +707,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
+    if (ctx->stream4) (void)hipStreamSynchronize(ctx->stream4);
     void* bufs[] = {ctx->d_in, ctx->d_pyr, ctx->d_tmp, ctx->d_cand, ctx->d_raw,
                     ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_stage,
                     ctx->d_mbuf};
@@ -706,6 +729,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
+    if (ctx->stream4) (void)hipStreamDestroy(ctx->stream4);
     delete ctx;
     return SIFT_OK;
 }

@@ -39,7 +39,9 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_g
                               unsigned cap, hipStream_t s);
 // Keypoint stages process the index range [*begin, *end) of their input
 // list (device counters), so a detect can run them in batches.
-hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s);
+// snap[w] = ctr[w] for w in [w0, w1)
+hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, int w0 = 0,
+                           int w1 = 4);
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s);

@@ -1319,12 +1319,13 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_g
     return hipGetLastError();
 }
 
-__global__ void k_snapshot(const unsigned* __restrict__ ctr, unsigned* __restrict__ snap) {
-    if (threadIdx.x < 4) snap[threadIdx.x] = ctr[threadIdx.x];
+__global__ void k_snapshot(const unsigned* __restrict__ ctr, unsigned* __restrict__ snap, int w0,
+                           int w1) {
+    if ((int)threadIdx.x >= w0 && (int)threadIdx.x < w1) snap[threadIdx.x] = ctr[threadIdx.x];
 }
 
-hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s) {
-    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(64), 0, s, ctr, snap);
+hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, int w0, int w1) {
+    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(64), 0, s, ctr, snap, w0, w1);
     return hipGetLastError();
 }
 

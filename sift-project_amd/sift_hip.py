@@ -19,7 +19,7 @@ from dataclasses import dataclass, fields
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsift_hip.so")
+LIB_PATH = os.environ.get("SIFT_HIP_LIB") or os.path.join(_HERE, "libsift_hip.so")
 
 KP_DTYPE = np.dtype(
     [
