@@ -135,6 +135,7 @@ def main() -> int:
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world)
+        from sift_dist import allgather_records
 
     W, H, B = args.width, args.height, args.batch
     ids = [rank * B + j for j in range(B)]
@@ -144,26 +145,37 @@ def main() -> int:
     ctx = Context(local_rank)
     params = SiftParams()
 
-    if world > 1:
-        from sift_dist import allgather_records
+    # N > 1: every step's records go to every rank (RCCL all-gather of the
+    # descriptor buffers). Warm-up steps use the exact two-phase
+    # all-gather and size the slots of the pipelined exchange, which then
+    # overlaps each step's all-gather with the next step's detection.
+    exchange = None
+    max_rows = 0
 
     def step() -> int:
+        nonlocal max_rows
         n_total = 0
         bufs = []
         for t in dev_imgs:
             kps, _ = ctx.detect_device(t.data_ptr(), W, H, 1, params)
             n_total += len(kps)
             if world > 1:
-                rec = torch.from_numpy(kps.view(np.uint8).reshape(-1, 168)).to(dev)
-                bufs.append(rec)
+                bufs.append(torch.from_numpy(kps.view(np.uint8).reshape(-1, 168)))
         if world > 1:
-            torch.cuda.synchronize()
-            allgather_records(bufs, ids, B)
+            max_rows = max(max_rows, n_total)
+            if exchange is None:
+                allgather_records([b.to(dev) for b in bufs], ids, B)
+            else:
+                exchange.push(bufs, ids)
         return n_total
 
     for _ in range(args.warmup):
         step()
     kp_per_image = ctx.counts()["final_n"]
+    if world > 1:
+        from sift_dist import RecordExchange, agree_capacity
+        exchange = RecordExchange(agree_capacity(max_rows, dev), dev)
+        step()  # one untimed pipelined step
 
     if world > 1:
         dist.barrier()
@@ -174,6 +186,8 @@ def main() -> int:
     kp_total = 0
     for _ in range(args.steps):
         kp_total += step()
+    if exchange is not None:
+        exchange.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -66,3 +66,120 @@ def allgather_records(local: Sequence[torch.Tensor], image_ids: Sequence[int],
             out[int(img_id)] = buf[off: off + n]
             off += n
     return out
+
+
+class RecordExchange:
+    """Pipelined all-gather of per-step record buffers for a steady stream of
+    batches (the multi-GPU bench path).
+
+    One collective per step, no count exchange and no host synchronisation:
+    every rank sends a fixed-capacity slot (`cap_rows` records of 168 B after
+    a 168-byte header row holding the image count and per-image
+    (image id, record count) pairs), with ``all_gather_into_tensor``
+    issued asynchronously on a side stream, so step i's exchange overlaps
+    step i+1's detection. Slots are double-buffered; a slot is refilled only
+    after the collective that last read it has completed. `cap_rows` must be
+    the same on every rank (see ``agree_capacity``). Every rank always takes
+    part in the same collective (no per-rank fallback that could diverge): a
+    slot that overflows is sent truncated with its true count, and
+    ``result`` raises for it; ``allgather_records`` is the exact two-phase
+    exchange for callers that cannot bound the counts.
+    """
+
+    MAX_IMAGES = 9  # (id, count) pairs in the 168-byte header row (int64 x 20)
+
+    def __init__(self, cap_rows: int, device: torch.device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.cap = int(cap_rows)
+        self.device = device
+        self.cuda = device.type == "cuda"
+        rows = self.cap + 1
+        pin = self.cuda
+        self.host = [torch.zeros((rows, RECORD_BYTES), dtype=torch.uint8, pin_memory=pin)
+                     for _ in range(2)]
+        self.dev = [torch.zeros((rows, RECORD_BYTES), dtype=torch.uint8, device=device)
+                    for _ in range(2)]
+        self.gathered = [torch.zeros((self.world * rows, RECORD_BYTES), dtype=torch.uint8,
+                                     device=device) for _ in range(2)]
+        self.stream = torch.cuda.Stream(device) if self.cuda else None
+        self.done = [None, None]  # per slot: event (cuda) / work handle (cpu)
+        self.work = [None, None]
+        self.step = 0
+
+    def _wait_slot(self, s: int) -> None:
+        if self.done[s] is not None:
+            self.done[s].synchronize() if self.cuda else self.work[s].wait()
+            self.done[s] = None
+            self.work[s] = None
+
+    def push(self, local: Sequence[torch.Tensor], image_ids: Sequence[int]) -> int:
+        """Start the exchange of this step's buffers (uint8 [n_i, 168], host);
+        returns the slot index whose `gathered` buffer will hold the result."""
+        if len(local) > self.MAX_IMAGES:
+            raise ValueError("too many images per step for the header row")
+        n_rows = sum(int(t.shape[0]) for t in local)
+        s = self.step & 1
+        self.step += 1
+        self._wait_slot(s)
+        h = self.host[s]
+        hdr = torch.zeros(2 + 2 * self.MAX_IMAGES, dtype=torch.int64)
+        hdr[0] = len(local)
+        hdr[1] = n_rows
+        for j, (t, i) in enumerate(zip(local, image_ids)):
+            hdr[2 + 2 * j] = int(i)
+            hdr[3 + 2 * j] = int(t.shape[0])
+        h[0, : hdr.numel() * 8] = hdr.view(torch.uint8)
+        off = 1
+        for t in local:  # a slot that overflows is truncated and flagged
+            n = min(int(t.shape[0]), self.cap + 1 - off)
+            h[off: off + n] = t[:n]
+            off += n
+        if self.cuda:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                self.dev[s][: off].copy_(h[: off], non_blocking=True)
+                self.work[s] = dist.all_gather_into_tensor(self.gathered[s], self.dev[s],
+                                                           group=self.group, async_op=True)
+                self.work[s].wait()  # orders the side stream after the collective
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+                self.done[s] = ev
+        else:
+            self.dev[s][: off] = h[: off]
+            self.work[s] = dist.all_gather_into_tensor(self.gathered[s], self.dev[s],
+                                                       group=self.group, async_op=True)
+            self.done[s] = self.work[s]
+        return s
+
+    def flush(self) -> None:
+        """Wait for every exchange in flight."""
+        for s in (0, 1):
+            self._wait_slot(s)
+
+    def result(self, s: int) -> Dict[int, torch.Tensor]:
+        """{image_id: uint8 [n, 168]} of a completed slot (call flush first)."""
+        rows = self.cap + 1
+        out: Dict[int, torch.Tensor] = {}
+        g = self.gathered[s].view(self.world, rows, RECORD_BYTES)
+        for r in range(self.world):
+            hdr = g[r, 0, : (2 + 2 * self.MAX_IMAGES) * 8].cpu().view(torch.int64)
+            if int(hdr[1]) > self.cap:
+                raise RuntimeError(f"rank {r} sent {int(hdr[1])} records into a slot of "
+                                   f"{self.cap}: raise the capacity (agree_capacity slack)")
+            off = 1
+            for j in range(int(hdr[0])):
+                n = int(hdr[3 + 2 * j])
+                out[int(hdr[2 + 2 * j])] = g[r, off: off + n]
+                off += n
+        return out
+
+
+def agree_capacity(local_max_rows: int, device: torch.device, slack: float = 1.5,
+                   group=None) -> int:
+    """Common slot capacity for RecordExchange: the largest per-rank record
+    count seen (e.g. over warm-up steps) times `slack`, rounded up to 1024."""
+    t = torch.tensor([int(local_max_rows)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    need = int(t.item() * slack) + 1
+    return (need + 1023) // 1024 * 1024

@@ -10,7 +10,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle_bind import OracleRun
-from sift_dist import RECORD_BYTES, allgather_records, shard
+from sift_dist import RECORD_BYTES, RecordExchange, agree_capacity, allgather_records, shard
 from sift_hip import synth_image
 
 
@@ -63,3 +63,62 @@ def test_shard_is_a_partition():
         seen = sorted(i for r in range(world) for i in shard(64, r, world))
         assert seen == list(range(64))
         assert all(len(shard(64, r, world)) == 64 // world for r in range(world))
+
+
+def _records(step, image, n):
+    g = np.random.default_rng(step * 1000 + image)
+    return g.integers(0, 256, size=(n, RECORD_BYTES), dtype=np.uint8)
+
+
+def _exchange_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids = shard(2 * world, rank, world)  # two images per rank
+        cap = agree_capacity(40 + 10 * rank, torch.device("cpu"), slack=1.0)
+        ex = RecordExchange(cap, torch.device("cpu"))
+        got = []
+        sizes = [(5, 7), (0, 3), (cap // 2, cap // 2 + 1)]  # last step overflows: fallback
+        for step, (a, b) in enumerate(sizes):
+            bufs = [torch.from_numpy(_records(step, ids[0], a + rank)),
+                    torch.from_numpy(_records(step, ids[1], b))]
+            s = ex.push(bufs, ids)
+            ex.flush()
+            try:
+                got.append({k: v.numpy().tobytes() for k, v in ex.result(s).items()})
+            except RuntimeError:
+                got.append(None)
+        out_q.put((rank, cap, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_record_exchange_gloo():
+    """Pipelined fixed-slot exchange (bench N > 1 path): every rank gets every
+    image's records; an overflowing slot is flagged on every receiver."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, cap, got = q.get(timeout=120)
+        res[r] = (cap, got)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0] == 1024  # max(40, 50) rounded up to 1024
+    for step, (a, b) in enumerate([(5, 7), (0, 3)]):
+        want = {}
+        for r in range(world):
+            ids = shard(2 * world, r, world)
+            want[ids[0]] = _records(step, ids[0], a + r).tobytes()
+            want[ids[1]] = _records(step, ids[1], b).tobytes()
+        for r in range(world):
+            assert res[r][1][step] == want
+    assert res[0][1][2] is None and res[1][1][2] is None
