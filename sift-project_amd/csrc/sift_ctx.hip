@@ -28,12 +28,18 @@ using namespace sift_amd;
 
 namespace {
 
-// device counter block: [0..3] live counters (candidates, refined, oriented),
-// [4..7] zeros, then per keypoint batch g a 4-word snapshot taken after its
-// extrema (the batch's candidate end and its record begins), then four
-// words per chain: work and done counters of orientation and descriptor
-constexpr int kCtrZeros = 4;
-constexpr int kCtrSnap = 8;
+// Keypoint lanes: batches alternate between two streams (C, D), each with
+// its own region of every keypoint array and its own counters, so the chains
+// of consecutive batches run concurrently (within a lane they are serial and
+// the snapshot ranges below stay contiguous).
+constexpr int kLanes = 2;
+// device counter block: [4L..4L+3] live counters of lane L (candidates,
+// refined, records), [8..11] zeros, then per keypoint batch g a 4-word
+// snapshot taken after its extrema (the batch's candidate end and its raw /
+// record begins, lane-local), then four words per chain: work and done
+// counters of orientation and descriptor
+constexpr int kCtrZeros = 4 * kLanes;
+constexpr int kCtrSnap = kCtrZeros + 4;
 constexpr int kCtrWork = kCtrSnap + 4 * (kMaxOctaves + 1);
 constexpr int kCtrWords = kCtrWork + 4 * (kMaxOctaves + 2);
 
@@ -104,12 +110,12 @@ struct sift_ctx {
     hipStream_t stream = nullptr;   // A: pyramid
     hipStream_t stream2 = nullptr;  // B: odd octaves of the pyramid
     hipStream_t stream3 = nullptr;  // C: extrema, refine, orientation, descriptor
-    hipStream_t stream4 = nullptr;  // D (optional): extrema, overlapping C's chains
+    hipStream_t stream4 = nullptr;  // D: keypoint chains of odd batches (lane 1)
     // persistent workgroups of orientation / descriptor: 768 = what fits at
     // once (3 per CU at the descriptor's 168 VGPRs); measured best of
     // 512/768/1024 (CU-masking stream C was measured slower)
     unsigned kp_wgs = 768;
-    int batch_px_log2 = 20;         // octaves of >= 2^this pixels get their own batch
+    int batch_px_log2 = 18;         // octaves of >= 2^this pixels get their own batch
     std::vector<hipEvent_t> sync_ev;
 
     double* d_in = nullptr;
@@ -124,9 +130,12 @@ struct sift_ctx {
     sift_kp* d_ori = nullptr;
     double* d_off0 = nullptr;
     float* d_df32 = nullptr;
+    // capacities per lane (each array holds kLanes regions of that size)
     unsigned cap_cand = 0, cap_raw = 0, cap_ori = 0, cap_off0 = 0, cap_df32 = 0;
+    int lanes = kLanes;  // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
+    unsigned lane_n[3][kLanes] = {};  // last detect: candidates, refined, records per lane
     unsigned* d_ctr = nullptr;
-    unsigned* h_ctr = nullptr;  // pinned
+    unsigned* h_ctr = nullptr;  // pinned, live counters of every lane
     PyrTable h_pt{};
     // per-call tables: pinned host staging -> one async copy -> device
     Stage* h_stage = nullptr;
@@ -200,6 +209,18 @@ int ensure_t(T** p, unsigned* cap, unsigned need) {
     *p = nullptr;
     *cap = 0;
     if (hipMalloc(p, (size_t)need * sizeof(T)) != hipSuccess) return SIFT_ERR_NOMEM;
+    *cap = need;
+    return SIFT_OK;
+}
+
+// kLanes regions of `need` elements each; *cap = per-lane capacity
+template <class T>
+int ensure_lanes(T** p, unsigned* cap, unsigned need) {
+    if (*cap >= need && *p) return SIFT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, (size_t)need * kLanes * sizeof(T)) != hipSuccess) return SIFT_ERR_NOMEM;
     *cap = need;
     return SIFT_OK;
 }
@@ -296,12 +317,12 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     // capacities for the variable-size stages; grown and re-run on overflow
     unsigned want_cand = (unsigned)std::min<size_t>(std::max<size_t>(g.sum_px / 32, 65536),
                                                    (size_t)1 << 28);
-    if ((st = ensure_t(&ctx->d_cand, &ctx->cap_cand, want_cand)) != SIFT_OK) return st;
-    if ((st = ensure_t(&ctx->d_raw, &ctx->cap_raw, ctx->cap_cand)) != SIFT_OK) return st;
-    if ((st = ensure_t(&ctx->d_ori, &ctx->cap_ori, 2 * ctx->cap_raw)) != SIFT_OK) return st;
-    if ((st = ensure_t(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
+    if ((st = ensure_lanes(&ctx->d_cand, &ctx->cap_cand, want_cand)) != SIFT_OK) return st;
+    if ((st = ensure_lanes(&ctx->d_raw, &ctx->cap_raw, ctx->cap_cand)) != SIFT_OK) return st;
+    if ((st = ensure_lanes(&ctx->d_ori, &ctx->cap_ori, 2 * ctx->cap_raw)) != SIFT_OK) return st;
+    if ((st = ensure_lanes(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
     if (out_desc_f32 &&
-        (st = ensure_t(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
+        (st = ensure_lanes(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
         return st;
 
     // Three streams (HIP's default is four hardware queues per process, and
@@ -312,6 +333,8 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     // keypoint work of octave 0 overlaps the pyramid of the smaller octaves,
     // which is latency-bound and leaves most of the chip idle.
     hipStream_t sA = ctx->stream, sB = ctx->stream2, sC = ctx->stream3, sD = ctx->stream4;
+    const int lanes = ctx->lanes;
+    hipStream_t lane_stream[kLanes] = {sC, sD};
     int ev_i = 0;
 
     SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sA));
@@ -366,40 +389,52 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         }
     const unsigned* zeros = ctx->d_ctr + kCtrZeros;
     auto snap = [&](int g) { return ctx->d_ctr + kCtrSnap + 4 * g; };
-    auto launch_extrema_range = [&](int o_begin, int o_end, hipStream_t sx) -> int {
+    auto launch_extrema_range = [&](int o_begin, int o_end, int L) -> int {
+        hipStream_t sx = lane_stream[L];
+        sift_extremum* cand = ctx->d_cand + (size_t)L * ctx->cap_cand;
+        unsigned* live = ctx->d_ctr + 4 * L;
         if (tiles) {
             const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
-            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, ctx->d_cand,
-                                              ctx->d_ctr + 0, ctx->cap_cand, sx));
+            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, cand,
+                                              live + 0, ctx->cap_cand, sx));
         } else {
             for (int o = o_begin; o < o_end; ++o)
                 SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
-                                                p->window_size, dp.threshold, ctx->d_cand,
-                                                ctx->d_ctr + 0, ctx->cap_cand, sx));
+                                                p->window_size, dp.threshold, cand, live + 0,
+                                                ctx->cap_cand, sx));
         }
         return SIFT_OK;
     };
     // records of every chain also go to the mapped export buffers, sized from
     // the largest record count seen so far (a larger one falls back to one
     // bulk download at the end, and grows them for the next call)
-    if ((st = ctx->exp_rec.ensure(std::max<size_t>(ctx->exp_rec.cap, 16384))) != SIFT_OK ||
+    if ((st = ctx->exp_rec.ensure(std::max<size_t>(ctx->exp_rec.cap, 16384 * kLanes))) !=
+            SIFT_OK ||
         (st = ctx->exp_off0.ensure(ctx->exp_rec.cap)) != SIFT_OK ||
         (st = ctx->exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
         return st;
     // poison: a range no launch published reads as "not exported"
     std::fill(ctx->exp_cnt.h, ctx->exp_cnt.h + ctx->exp_cnt.cap, 0xFFFFFFFFu);
+    // lane L exports its records (lane-local index i) to exp_rec[L * exp_lane + i]
+    const unsigned exp_lane = (unsigned)(ctx->exp_rec.cap / kLanes);
     int n_chains = 0;
-    // extrema over [o_begin, o_end) then refine -> orientation -> descriptor.
-    // `begin` (a counter snapshot taken right after the extrema) holds this
-    // batch's candidate end and its raw / record begins; candidates start at
-    // cand_begin (the previous batch's snapshot). The re-run passes nullptr.
-    // With stream D the extrema of batch g run there as soon as their levels
-    // exist, overlapping the keypoint chain of batch g-1 on C: D snapshots the
-    // candidate end, C (after its previous chain) the raw / record begins.
-    auto run_chain = [&](int o_begin, int o_end, const unsigned* cand_begin,
+    std::vector<int> chain_lane;
+    // extrema over [o_begin, o_end) then refine -> orientation -> descriptor,
+    // on lane L. `begin` (a counter snapshot taken right after the extrema)
+    // holds this batch's candidate end and its raw / record begins; candidates
+    // start at cand_begin (the lane's previous batch's snapshot). The re-run
+    // passes nullptr (lane 0, live counters).
+    auto run_chain = [&](int L, int o_begin, int o_end, const unsigned* cand_begin,
                          unsigned* begin) -> int {
-        const bool split = sD && begin;
         const int ci = n_chains++;
+        chain_lane.push_back(L);
+        hipStream_t sx = lane_stream[L];
+        unsigned* live = ctx->d_ctr + 4 * L;
+        sift_extremum* cand = ctx->d_cand + (size_t)L * ctx->cap_cand;
+        RawKp* raw = ctx->d_raw + (size_t)L * ctx->cap_raw;
+        sift_kp* recs = ctx->d_ori + (size_t)L * ctx->cap_ori;
+        double* off0 = ctx->d_off0 + (size_t)L * ctx->cap_ori;
+        float* df32 = out_desc_f32 ? ctx->d_df32 + (size_t)L * ctx->cap_ori * 128 : nullptr;
         unsigned* work = ctx->d_ctr + kCtrWork + 4 * ci;
         while ((int)ctx->chain_ev.size() <= ci) {
             hipEvent_t e;
@@ -407,45 +442,35 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
                 return SIFT_ERR_HIP;
             ctx->chain_ev.push_back(e);
         }
-        const ExportSink ex{ctx->exp_rec.d, ctx->exp_off0.d, ctx->exp_cnt.d + 2 * ci,
-                            (unsigned)ctx->exp_rec.cap};
-        int st2 = launch_extrema_range(o_begin, o_end, split ? sD : sC);
+        const ExportSink ex{ctx->exp_rec.d + (size_t)L * exp_lane,
+                            ctx->exp_off0.d + (size_t)L * exp_lane, ctx->exp_cnt.d + 2 * ci,
+                            exp_lane};
+        int st2 = launch_extrema_range(o_begin, o_end, L);
         if (st2 != SIFT_OK) return st2;
-        if (split) {
-            SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sD, 0, 1));
-            hipEvent_t ext_done = sync_event(ctx, ev_i++);
-            if (!ext_done) return SIFT_ERR_HIP;
-            SIFT_HIP_TRY(hipEventRecord(ext_done, sD));
-            SIFT_HIP_TRY(hipStreamWaitEvent(sC, ext_done, 0));
-            SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC, 1, 3));
-        } else if (begin) {
-            SIFT_HIP_TRY(launch_snapshot(ctx->d_ctr, begin, sC));
-        }
+        if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 4));
         const unsigned* b = begin ? begin : zeros;
-        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, ctx->d_cand, cand_begin,
-                                   begin ? begin : ctx->d_ctr + 0, ctx->cap_cand, ctx->d_raw,
-                                   ctx->d_ctr + 1, ctx->cap_raw, sC));
-        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, ctx->d_raw, b + 1, ctx->d_ctr + 1, ctx->cap_raw,
-                                   ctx->d_ori, ctx->d_off0, ctx->d_ctr + 2, ctx->cap_ori, work,
-                                   ctx->kp_wgs, sC));
-        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, ctx->d_ori, ctx->d_off0, b + 2,
-                                       ctx->d_ctr + 2, ctx->cap_ori,
-                                       out_desc_f32 ? ctx->d_df32 : nullptr, work + 2, ex,
-                                       ctx->kp_wgs, sC));
-        SIFT_HIP_TRY(hipEventRecord(ctx->chain_ev[ci], sC));
+        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, cand, cand_begin, begin ? begin : live + 0,
+                                   ctx->cap_cand, raw, live + 1, ctx->cap_raw, sx));
+        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, raw, b + 1, live + 1, ctx->cap_raw, recs, off0,
+                                   live + 2, ctx->cap_ori, work, ctx->kp_wgs, sx));
+        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, recs, off0, b + 2, live + 2, ctx->cap_ori,
+                                       df32, work + 2, ex, ctx->kp_wgs, sx));
+        SIFT_HIP_TRY(hipEventRecord(ctx->chain_ev[ci], sx));
         return SIFT_OK;
     };
     int n_batches = 0;
-    // batch g: octaves [o_begin, o_end), whose levels were enqueued on `sps`
+    // batch g (lane g % lanes): octaves [o_begin, o_end), whose levels were
+    // enqueued on `sps`
     auto batch = [&](int o_begin, int o_end, std::initializer_list<hipStream_t> sps) -> int {
         const int gb = n_batches++;
+        const int L = gb % lanes;
         for (hipStream_t sp : sps) {
             hipEvent_t pyr_done = sync_event(ctx, ev_i++);
             if (!pyr_done) return SIFT_ERR_HIP;
             SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
-            SIFT_HIP_TRY(hipStreamWaitEvent(sD ? sD : sC, pyr_done, 0));
+            SIFT_HIP_TRY(hipStreamWaitEvent(lane_stream[L], pyr_done, 0));
         }
-        return run_chain(o_begin, o_end, gb == 0 ? zeros : snap(gb - 1), snap(gb));
+        return run_chain(L, o_begin, o_end, gb < lanes ? zeros : snap(gb - lanes), snap(gb));
     };
     // The pyramid alternates between two streams, octave o on pyr[o % 2]:
     // octave o+1 only needs the decimated level `intervals` of octave o, so it
@@ -486,18 +511,23 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
                                         ctx->d_taps, so, e0, e1));
     }
     if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
-    // stream B joins A (the ctx's public stream) before the call returns
+    // stream B joins A (the ctx's public stream) before the call returns, and
+    // lane D joins C (the counters are read back on C)
     {
         hipEvent_t j = sync_event(ctx, ev_i++);
         if (!j) return SIFT_ERR_HIP;
         SIFT_HIP_TRY(hipEventRecord(j, sB));
         SIFT_HIP_TRY(hipStreamWaitEvent(sA, j, 0));
+        hipEvent_t jd = sync_event(ctx, ev_i++);
+        if (!jd) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(hipEventRecord(jd, sD));
+        SIFT_HIP_TRY(hipStreamWaitEvent(sC, jd, 0));
     }
 
     // ---- finalise each batch on the host while the device runs the next:
     // sizes with glibc pow and a sorted run per batch, from the exported
     // records (sift.cpp:20-24, 427-429)
-    SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
+    SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * kLanes * sizeof(unsigned),
                                 hipMemcpyDeviceToHost, sC));
     clk::time_point t_enq = clk::now(), t_wait;
     bool exported = true;
@@ -507,13 +537,15 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     for (int ci = 0; ci < n_chains; ++ci) {
         SIFT_HIP_TRY(hipEventSynchronize(ctx->chain_ev[ci]));
         const unsigned b = ctx->exp_cnt.h[2 * ci], e = ctx->exp_cnt.h[2 * ci + 1];
-        if (e > ctx->exp_rec.cap || b > e) {
+        if (e > exp_lane || b > e) {
             exported = false;
             break;
         }
-        host_sizes(p, ctx->exp_rec.h, ctx->exp_off0.h, b, e);
+        const unsigned base = (unsigned)chain_lane[ci] * exp_lane;
+        host_sizes(p, ctx->exp_rec.h, ctx->exp_off0.h, base + b, base + e);
         ctx->run_start.push_back(n_keys);
-        host_sort_run(ctx->exp_rec.h, b, e, ctx->fin_ws.all.data() + n_keys, &ctx->fin_ws);
+        host_sort_run(ctx->exp_rec.h, base + b, base + e, ctx->fin_ws.all.data() + n_keys,
+                      &ctx->fin_ws);
         n_keys += e - b;
     }
     ctx->run_start.push_back(n_keys);
@@ -525,13 +557,19 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
             SIFT_HIP_TRY(hipStreamSynchronize(sC));
             n_chains = 0;
-            if ((st = run_chain(0, g.octaves, zeros, nullptr)) != SIFT_OK) return st;
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * sizeof(unsigned),
+            chain_lane.clear();
+            if ((st = run_chain(0, 0, g.octaves, zeros, nullptr)) != SIFT_OK) return st;
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
         }
         SIFT_HIP_TRY(hipStreamSynchronize(sC));
         t_wait = clk::now();
-        const unsigned nc = ctx->h_ctr[0], nr = ctx->h_ctr[1], no = ctx->h_ctr[2];
+        unsigned nc = 0, nr = 0, no = 0;  // largest per-lane counts
+        for (int L = 0; L < kLanes; ++L) {
+            nc = std::max(nc, ctx->h_ctr[4 * L]);
+            nr = std::max(nr, ctx->h_ctr[4 * L + 1]);
+            no = std::max(no, ctx->h_ctr[4 * L + 2]);
+        }
         if (nc <= ctx->cap_cand && nr <= ctx->cap_raw && no <= ctx->cap_ori) break;
         if (attempt >= 3) return SIFT_ERR_NOMEM;
         // grow every stage that overflowed (refine/orient counts are lower
@@ -539,35 +577,54 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
         const unsigned nc2 = std::max(ctx->cap_cand, nc) * 2u;
         const unsigned nr2 = std::max(std::max(ctx->cap_raw, nr) * 2u, nc2);
         const unsigned no2 = std::max(std::max(ctx->cap_ori, no) * 2u, 2u * nr2);
-        if ((st = ensure_t(&ctx->d_cand, &ctx->cap_cand, nc2)) != SIFT_OK) return st;
-        if ((st = ensure_t(&ctx->d_raw, &ctx->cap_raw, nr2)) != SIFT_OK) return st;
-        if ((st = ensure_t(&ctx->d_ori, &ctx->cap_ori, no2)) != SIFT_OK) return st;
-        if ((st = ensure_t(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
+        if ((st = ensure_lanes(&ctx->d_cand, &ctx->cap_cand, nc2)) != SIFT_OK) return st;
+        if ((st = ensure_lanes(&ctx->d_raw, &ctx->cap_raw, nr2)) != SIFT_OK) return st;
+        if ((st = ensure_lanes(&ctx->d_ori, &ctx->cap_ori, no2)) != SIFT_OK) return st;
+        if ((st = ensure_lanes(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
         if (out_desc_f32 &&
-            (st = ensure_t(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
+            (st = ensure_lanes(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
             return st;
     }
 
-    const unsigned n_ori = ctx->h_ctr[2];
+    unsigned n_lane[kLanes];  // records per lane
+    unsigned n_ori = 0;
+    for (int L = 0; L < kLanes; ++L) {
+        n_lane[L] = ctx->h_ctr[4 * L + 2];
+        ctx->lane_n[0][L] = ctx->h_ctr[4 * L];
+        ctx->lane_n[1][L] = ctx->h_ctr[4 * L + 1];
+        ctx->lane_n[2][L] = n_lane[L];
+        n_ori += n_lane[L];
+    }
     if (exported && n_keys != n_ori) exported = false;
     const sift_kp* rec_src = ctx->exp_rec.h;
+    // host position of lane L's record i: exported, L * exp_lane + i; after a
+    // bulk download, the lanes are concatenated
+    size_t host_base[kLanes];
+    for (int L = 0, acc = 0; L < kLanes; acc += n_lane[L], ++L)
+        host_base[L] = exported ? (size_t)L * exp_lane : (size_t)acc;
     if (!exported) {  // bulk download of every record
         if ((st = ctx->h_ori.ensure(n_ori)) != SIFT_OK) return st;
         if ((st = ctx->h_off0.ensure(n_ori)) != SIFT_OK) return st;
-        if (n_ori) {
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.p, ctx->d_ori, n_ori * sizeof(sift_kp),
-                                        hipMemcpyDeviceToHost, sC));
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.p, ctx->d_off0, n_ori * sizeof(double),
-                                        hipMemcpyDeviceToHost, sC));
+        for (int L = 0; L < kLanes; ++L) {
+            if (!n_lane[L]) continue;
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.p + host_base[L],
+                                        ctx->d_ori + (size_t)L * ctx->cap_ori,
+                                        n_lane[L] * sizeof(sift_kp), hipMemcpyDeviceToHost, sC));
+            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.p + host_base[L],
+                                        ctx->d_off0 + (size_t)L * ctx->cap_ori,
+                                        n_lane[L] * sizeof(double), hipMemcpyDeviceToHost, sC));
         }
         rec_src = ctx->h_ori.p;
     }
     if (out_desc_f32) {
-        if ((st = ctx->h_df32.ensure((size_t)n_ori * 128)) != SIFT_OK) return st;
-        if (n_ori)
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.p, ctx->d_df32,
-                                        (size_t)n_ori * 128 * sizeof(float),
-                                        hipMemcpyDeviceToHost, sC));
+        const size_t span = exported ? ctx->exp_rec.cap : (size_t)n_ori;
+        if ((st = ctx->h_df32.ensure(std::max<size_t>(span, 1) * 128)) != SIFT_OK) return st;
+        for (int L = 0; L < kLanes; ++L)
+            if (n_lane[L])
+                SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.p + host_base[L] * 128,
+                                            ctx->d_df32 + (size_t)L * ctx->cap_ori * 128,
+                                            (size_t)n_lane[L] * 128 * sizeof(float),
+                                            hipMemcpyDeviceToHost, sC));
     }
     SIFT_HIP_TRY(hipStreamSynchronize(sC));
     const auto t_copy = clk::now();
@@ -585,7 +642,7 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
 
     // clean_keypoints: merge the sorted runs and unique (or all of it, after
     // a bulk download), in the g++-built layer
-    ctx->keep.resize(n_ori);
+    ctx->keep.resize(std::max<unsigned>(n_ori, 1));
     size_t n;
     if (exported) {
         n = host_merge_unique(ctx->exp_rec.h, ctx->fin_ws.all.data(), ctx->run_start,
@@ -593,9 +650,10 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     } else {
         n = host_finalize(p, ctx->h_ori.p, ctx->h_off0.p, n_ori, ctx->keep.data(),
                           &ctx->fin_ws);
-        // the next call exports this many records
-        if (n_ori > ctx->exp_rec.cap) {
-            const size_t want = (size_t)n_ori + n_ori / 2;
+        // the next call exports this many records per lane
+        const unsigned lane_max = std::max(n_lane[0], n_lane[1]);
+        if (lane_max > exp_lane) {
+            const size_t want = ((size_t)lane_max + lane_max / 2) * kLanes;
             if ((st = ctx->exp_rec.ensure(want)) != SIFT_OK ||
                 (st = ctx->exp_off0.ensure(want)) != SIFT_OK)
                 return st;
@@ -627,8 +685,8 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     *out_n = n;
     if (out_desc_f32) *out_desc_f32 = df;
 
-    ctx->counts.extrema = ctx->h_ctr[0];
-    ctx->counts.refined = ctx->h_ctr[1];
+    ctx->counts.extrema = (int64_t)ctx->lane_n[0][0] + ctx->lane_n[0][1];
+    ctx->counts.refined = (int64_t)ctx->lane_n[1][0] + ctx->lane_n[1][1];
     ctx->counts.oriented = n_ori;
     ctx->counts.final_n = (int64_t)n;
     ctx->counts.octaves = g.octaves;
@@ -676,19 +734,14 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::atoi(e);
     if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
     if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) ctx->batch_px_log2 = std::atoi(e);
-    const char* ext_stream = std::getenv("SIFT_EXT_STREAM");
-    if (ext_stream && std::atoi(ext_stream) > 0 &&
-        hipStreamCreateWithPriority(&ctx->stream4, hipStreamNonBlocking,
-                                    std::atoi(ext_stream) > 1 ? prio_hi : prio_lo) != hipSuccess) {
-        sift_hip_destroy(ctx);
-        return SIFT_ERR_HIP;
-    }
-    if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 20;
+    if (const char* e = std::getenv("SIFT_KP_LANES")) ctx->lanes = std::atoi(e) == 1 ? 1 : kLanes;
+    if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 18;
     if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stream4, hipStreamNonBlocking, prio_lo) != hipSuccess ||
         hipMalloc(&ctx->d_ctr, kCtrWords * sizeof(unsigned)) != hipSuccess ||
-        hipHostMalloc(&ctx->h_ctr, 4 * sizeof(unsigned)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_ctr, 4 * kLanes * sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&ctx->h_stage, sizeof(Stage)) != hipSuccess ||
         hipMalloc(&ctx->d_stage, sizeof(Stage)) != hipSuccess ||
         prepare_kernel_attributes() != hipSuccess) {
@@ -907,9 +960,11 @@ int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out, size_t cap, si
     if (!host_out) return SIFT_OK;
     if (cap < n) return SIFT_ERR_ARG;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
-    if (n)
-        SIFT_HIP_TRY(hipMemcpyAsync(host_out, ctx->d_cand, n * sizeof(sift_extremum),
-                                    hipMemcpyDeviceToHost, ctx->stream));
+    for (int L = 0, off = 0; L < kLanes; off += ctx->lane_n[0][L], ++L)
+        if (ctx->lane_n[0][L])
+            SIFT_HIP_TRY(hipMemcpyAsync(host_out + off, ctx->d_cand + (size_t)L * ctx->cap_cand,
+                                        ctx->lane_n[0][L] * sizeof(sift_extremum),
+                                        hipMemcpyDeviceToHost, ctx->stream));
     SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return SIFT_OK;
 }
@@ -922,9 +977,12 @@ int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t*
     if (!d_dst) return SIFT_OK;
     if (cap < n) return SIFT_ERR_ARG;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
-    if (n)
-        SIFT_HIP_TRY(hipMemcpyAsync(d_dst, ctx->d_ori, n * sizeof(sift_kp),
-                                    hipMemcpyDeviceToDevice, ctx->stream));
+    for (int L = 0, off = 0; L < kLanes; off += ctx->lane_n[2][L], ++L)
+        if (ctx->lane_n[2][L])
+            SIFT_HIP_TRY(hipMemcpyAsync(static_cast<sift_kp*>(d_dst) + off,
+                                        ctx->d_ori + (size_t)L * ctx->cap_ori,
+                                        ctx->lane_n[2][L] * sizeof(sift_kp),
+                                        hipMemcpyDeviceToDevice, ctx->stream));
     SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return SIFT_OK;
 }
