@@ -111,10 +111,10 @@ struct sift_ctx {
     hipStream_t stream2 = nullptr;  // B: odd octaves of the pyramid
     hipStream_t stream3 = nullptr;  // C: extrema, refine, orientation, descriptor
     hipStream_t stream4 = nullptr;  // D: keypoint chains of odd batches (lane 1)
-    // persistent workgroups of orientation / descriptor: 768 = what fits at
-    // once (3 per CU at the descriptor's 168 VGPRs); measured best of
-    // 512/768/1024 (CU-masking stream C was measured slower)
-    unsigned kp_wgs = 768;
+    // persistent workgroups of orientation / descriptor per launch: 512 (two
+    // per CU; with two keypoint lanes in flight this leaves room for the
+    // small octaves' blurs); measured best of 256/384/512/768/1024
+    unsigned kp_wgs = 512;
     int batch_px_log2 = 18;         // octaves of >= 2^this pixels get their own batch
     std::vector<hipEvent_t> sync_ev;
 
