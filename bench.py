@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from sift_hip import Context, SiftParams, synth_image  # noqa: E402
+from sift_hip import INPUT_F64_DEVICE, INPUT_F64_HOST, Context, SiftParams, synth_image  # noqa: E402
 
 METRIC = ("keypoints/sec (detect+describe) on 1920×1080; Gaussian-pyramid HBM GB/s vs peak")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -107,11 +107,78 @@ def matcher_bench(ctx, dev, kps_a, W, H, params, cpu_seconds: float) -> dict:
     return out
 
 
+def pipelined(ctx, submit, n_steps: int):
+    """Run n_steps jobs with job k+1 submitted before job k is fetched;
+    returns (keypoints of all jobs, elapsed s, per-job keypoint counts)."""
+    kp = 0
+    t0 = time.perf_counter()
+    t = submit(0)
+    for k in range(n_steps):
+        t_next = submit(k + 1) if k + 1 < n_steps else None
+        kps, _ = ctx.fetch(t)
+        kp += sum(len(x) for x in kps)
+        t = t_next
+    return kp, time.perf_counter() - t0
+
+
+def extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params, seconds: float) -> dict:
+    """Secondary measurements at N=1 (after the timed region): single-image
+    latency (sync), the reference API path from a host Image buffer (sync and
+    pipelined), an 8-image job per step (BASELINE config 4 layout on one GPU),
+    and the host-side phase times of a detect."""
+    out = {}
+    img_dev = dev_imgs[0].data_ptr()
+    img_host = host_imgs[0]
+
+    def timed_loop(fn, min_s):
+        fn()
+        n, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= min_s and n >= 5:
+                return dt / n
+
+    lat = timed_loop(lambda: ctx.detect_device(img_dev, W, H, 1, params), seconds)
+    kp1 = ctx.counts()["final_n"]
+    phases = ctx.host_timing()
+    out["latency"] = {"ms_per_image": lat * 1e3, "keypoints_per_s": kp1 / lat,
+                      "note": "one synchronous detect per image (input in HBM), no pipelining"}
+    api = timed_loop(lambda: ctx.detect(img_host, params), seconds)
+    n_api = max(5, int(seconds / api))
+    kp_api, t_api = pipelined(
+        ctx, lambda k: ctx.submit([img_host], INPUT_F64_HOST, W, H, 1, params), n_api)
+    out["api"] = {
+        "value": kp_api / t_api, "unit": "keypoints/s", "ms_per_image": t_api / n_api * 1e3,
+        "sync_ms_per_image": api * 1e3, "sync_value": kp1 / api,
+        "path": "sift_hip_submit/fetch from a host Image buffer (float64 HWC, reference "
+                "image_io.hh:22-26): integer-valued -> packed to u8 on 8 host threads, pinned "
+                "staging, async H2D, u8->f64 on device; pipelined one job ahead (value) and "
+                "synchronous per call (sync_*), PCIe included"}
+    B = 8
+    batch_imgs = [synth_image(W, H, 1, seed=42 + i) for i in range(B)]
+    bt = [torch.from_numpy(a).to(dev) for a in batch_imgs]
+    torch.cuda.synchronize()
+    ptrs = [t.data_ptr() for t in bt]
+    sub = lambda k: ctx.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params)  # noqa: E731
+    pipelined(ctx, sub, 3)
+    one = timed_loop(lambda: ctx.fetch(sub(0)), 0.5)
+    n_b = max(5, int(seconds / one))
+    kp_b, t_b = pipelined(ctx, sub, n_b)
+    out["batch8"] = {"images_per_s": n_b * B / t_b, "ms_per_image": t_b / (n_b * B) * 1e3,
+                     "keypoints_per_s": kp_b / t_b, "jobs": n_b,
+                     "note": "8 synthetic 1920x1080 images (seeds 42..49) per job, one batched "
+                             "launch per kernel, jobs pipelined one ahead, inputs in HBM"}
+    out["host_phases_ms"] = phases
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=2500)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1, help="images per GPU per step")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -119,6 +186,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-matcher", action="store_true",
                     help="skip the matcher measurement (SURVEY §8f row 1)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the latency / API / batch8 legs")
+    ap.add_argument("--extra-seconds", type=float, default=2.0)
     ap.add_argument("--no-events", action="store_true",
                     help="skip the per-launch HIP events of the pyramid roofline")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "blur_traffic.json"),
@@ -152,16 +222,21 @@ def main() -> int:
     exchange = None
     max_rows = 0
 
-    def step() -> int:
+    # A step = one job over this rank's B images (inputs resident in HBM).
+    # Steps are pipelined: step k+1's job is submitted before step k's
+    # records are fetched, so the device runs k+1's pyramid while the host
+    # sorts k's records. Every step's work is inside the timed region.
+    ptrs = [t.data_ptr() for t in dev_imgs]
+
+    def submit():
+        return ctx.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params)
+
+    def finish(ticket) -> int:
         nonlocal max_rows
-        n_total = 0
-        bufs = []
-        for t in dev_imgs:
-            kps, _ = ctx.detect_device(t.data_ptr(), W, H, 1, params)
-            n_total += len(kps)
-            if world > 1:
-                bufs.append(torch.from_numpy(kps.view(np.uint8).reshape(-1, 168)))
+        kps, _ = ctx.fetch(ticket)
+        n_total = sum(len(k) for k in kps)
         if world > 1:
+            bufs = [torch.from_numpy(k.view(np.uint8).reshape(-1, 168)) for k in kps]
             max_rows = max(max_rows, n_total)
             if exchange is None:
                 allgather_records([b.to(dev) for b in bufs], ids, B)
@@ -169,13 +244,21 @@ def main() -> int:
                 exchange.push(bufs, ids)
         return n_total
 
-    for _ in range(args.warmup):
-        step()
-    kp_per_image = ctx.counts()["final_n"]
+    def run(n_steps: int) -> int:
+        kp = 0
+        t = submit()
+        for k in range(n_steps):
+            t_next = submit() if k + 1 < n_steps else None
+            kp += finish(t)
+            t = t_next
+        return kp
+
+    run(max(1, args.warmup))
+    kp_per_image = ctx.counts()["final_n"] // B
     if world > 1:
         from sift_dist import RecordExchange, agree_capacity
         exchange = RecordExchange(agree_capacity(max_rows, dev), dev)
-        step()  # one untimed pipelined step
+        run(1)  # one untimed pipelined step
 
     if world > 1:
         dist.barrier()
@@ -183,9 +266,7 @@ def main() -> int:
     ctx.set_profiling(not args.no_events)
     ctx.blur_profile(reset=True)
     t0 = time.perf_counter()
-    kp_total = 0
-    for _ in range(args.steps):
-        kp_total += step()
+    kp_total = run(args.steps)
     if exchange is not None:
         exchange.flush()
     torch.cuda.synchronize()
@@ -248,6 +329,10 @@ def main() -> int:
             },
             "roofline": roofline,
         }
+        out["timed_region_s"] = elapsed
+        if world == 1 and not args.no_extra:
+            out.update(extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params,
+                                  args.extra_seconds))
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(host_imgs[0], args.cpu_seconds)
         if world == 1 and not args.no_matcher:

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SIFT_HIP_ABI_VERSION 1
+#define SIFT_HIP_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define SIFT_OK 0
@@ -97,8 +97,9 @@ typedef struct sift_ctx sift_ctx;
 /* Fill *p with the reference defaults (sift.hh:65-71). */
 void sift_params_default(sift_params* p);
 
-/* Create a context bound to HIP device `device`: owns one HIP stream and a
- * device arena that grows to the largest image seen. */
+/* Create a context bound to HIP device `device`: owns four HIP streams and
+ * SIFT_MAX_INFLIGHT job slots, each with a device arena that grows to the
+ * largest job seen. */
 int sift_hip_create(int device, sift_ctx** out);
 int sift_hip_destroy(sift_ctx* ctx);
 
@@ -124,6 +125,52 @@ int sift_hip_detect_device(sift_ctx* ctx, const double* d_hwc, int w, int h,
 
 void sift_hip_free(void* p);
 const char* sift_hip_strerror(int status);
+
+/* ---- jobs: batches of images, pipelined ------------------------------- */
+/*
+ * A job is 1..SIFT_MAX_BATCH images of the same w x h x c and parameters,
+ * each processed exactly as detect_keypoints_and_descriptors would
+ * (reference sift.cpp:712-776 is a pure function of one image); every kernel
+ * of a job covers all its images in one launch. Up to SIFT_MAX_INFLIGHT jobs
+ * can be in flight per context: submit job k+1 before waiting on job k and
+ * the device works on k+1 while the host finalises k.
+ *
+ * Input kinds: the reference Image buffer (interleaved HWC doubles,
+ * image_io.cpp:81-92) in host or device memory, or the 8-bit pixels stb
+ * decodes (image_io.cpp:20-35; converted to double on the device, exactly).
+ * Host double images whose values are all integers 0..255 (every
+ * stb-decoded Image) are uploaded as bytes; the results are identical.
+ * Device / host input buffers must stay valid until sift_hip_wait returns.
+ */
+#define SIFT_INPUT_F64_HOST 0
+#define SIFT_INPUT_F64_DEVICE 1
+#define SIFT_INPUT_U8_HOST 2
+#define SIFT_INPUT_U8_DEVICE 3
+#define SIFT_MAX_BATCH 16
+#define SIFT_MAX_INFLIGHT 2
+
+/* Enqueue a job; *ticket identifies it. SIFT_ERR_STATE when
+ * SIFT_MAX_INFLIGHT jobs are already in flight (wait/fetch one first). */
+int sift_hip_submit(sift_ctx* ctx, const void* const* images, int n_images, int input_kind,
+                    int w, int h, int c, const sift_params* p, int want_desc_f32,
+                    int* ticket);
+
+/* Block until the job is finalised (sorted and de-duplicated per image, as
+ * clean_keypoints, sift.cpp:20-24); counts[b] (n_images entries, optional)
+ * = keypoints of image b, *total = their sum. */
+int sift_hip_wait(sift_ctx* ctx, int ticket, size_t* counts, size_t* total);
+
+/* Copy the job's keypoints into caller storage (total records, image-major:
+ * image 0's sorted list, then image 1's, ...) and, if requested at submit,
+ * total*128 normalised descriptor floats; releases the job. out == NULL
+ * releases it without copying. Waits first if needed. */
+int sift_hip_fetch(sift_ctx* ctx, int ticket, sift_kp* out, float* desc_f32);
+
+/* submit + wait + fetch into library-allocated storage (sift_hip_free):
+ * *out_kps image-major, counts[b] per image. */
+int sift_hip_detect_batch(sift_ctx* ctx, const void* const* images, int n_images,
+                          int input_kind, int w, int h, int c, const sift_params* p,
+                          sift_kp** out_kps, size_t* counts, float** out_desc_f32);
 
 /* ---- matcher -------------------------------------------------------------- */
 /*
@@ -151,7 +198,9 @@ int sift_hip_match_device(sift_ctx* ctx, const sift_kp* d_kps1, size_t n1,
                           const sift_kp* d_kps2, size_t n2, double ratio_threshold,
                           sift_match_pair** out, size_t* n_out);
 
-/* ---- introspection of the last detect (tests, bench, multi-GPU) -------- */
+/* ---- introspection of the last finalised job (tests, bench, multi-GPU) -- */
+/* (valid until a later submit reuses that job's slot; counts sum over the
+ * job's images) */
 
 /* Pipeline counts of the last detect: extrema candidates, refined
  * keypoints, oriented keypoints (pre-dedup), final keypoints, octaves. */

@@ -74,16 +74,24 @@ std::vector<Keypoint> detect_keypoints_and_descriptors(
     p.ori_sigma_factor = ori_sigma_factor;
     p.desc_scale_factor = desc_scale_factor;
 
-    sift_kp* raw = nullptr;
+    // one job: the Image buffer goes up through pinned staging (as bytes when
+    // it holds stb-decoded integers), and the sorted records are copied once,
+    // straight into the returned vector
+    sift_ctx* ctx = thread_context();
+    const void* src = img.data.data();
+    int ticket = 0;
     size_t n = 0;
-    const int st = sift_hip_detect(thread_context(), img.data.data(), img.width, img.height,
-                                   img.channels, &p, &raw, &n, nullptr);
+    int st = sift_hip_submit(ctx, &src, 1, SIFT_INPUT_F64_HOST, img.width, img.height,
+                             img.channels, &p, 0, &ticket);
+    if (st == SIFT_OK) st = sift_hip_wait(ctx, ticket, nullptr, &n);
+    std::vector<Keypoint> out;
+    if (st == SIFT_OK) {
+        out.resize(n);
+        st = sift_hip_fetch(ctx, ticket, reinterpret_cast<sift_kp*>(out.data()), nullptr);
+    }
     if (st != SIFT_OK)
         throw std::runtime_error(std::string("detect_keypoints_and_descriptors: ") +
                                  sift_hip_strerror(st));
-    std::unique_ptr<sift_kp, void (*)(void*)> guard(raw, sift_hip_free);
-    std::vector<Keypoint> out(n);
-    if (n) std::memcpy(static_cast<void*>(out.data()), raw, n * sizeof(sift_kp));
 
     // the reference writes keypoints.png on every call (sift.cpp:765-768)
     if (env_flag("SIFT_AMD_KEYPOINTS_PNG", true)) {

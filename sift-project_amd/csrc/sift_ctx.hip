@@ -7,9 +7,18 @@
 // (sift.cpp:132-137), the level sigmas (sift.cpp:143-155), the blur taps
 // (image.cpp:226-235), the final keypoint size (std::pow, sift.cpp:427-429)
 // and clean_keypoints (std::sort + std::unique, sift.cpp:20-24). Everything
-// per-pixel and per-keypoint runs in the HIP kernels of sift_kernels.hip,
-// enqueued on three streams with no host synchronisation until the counters are
-// read back at the end.
+// per-pixel and per-keypoint runs in the HIP kernels of sift_kernels.hip.
+//
+// Jobs. A job is 1..kMaxImages images of one shape and one parameter set
+// (the reference function is pure per image, sift.cpp:712-776, so images
+// are independent); every kernel of a job covers all its images in one
+// launch (blockIdx.z / .y = image), so a batch of 8 1080p images costs the
+// launches of one. A context owns kSlots job slots, each with its own
+// pyramid arena, keypoint arrays, counters, staging and export buffers, so
+// job k+1 can be enqueued (submit) before job k is finalised on the host
+// (wait / fetch): the device runs job k+1's pyramid while the host sorts job
+// k's records. Completion is tracked with per-slot events only — no stream
+// synchronisation on the pipelined path.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,32 +37,40 @@ using namespace sift_amd;
 
 namespace {
 
+using clk = std::chrono::steady_clock;
+
 // Keypoint lanes: batches alternate between two streams (C, D), each with
 // its own region of every keypoint array and its own counters, so the chains
 // of consecutive batches run concurrently (within a lane they are serial and
 // the snapshot ranges below stay contiguous).
 constexpr int kLanes = 2;
-// device counter block: [4L..4L+3] live counters of lane L (candidates,
-// refined, records), [8..11] zeros, then per keypoint batch g a 4-word
-// snapshot taken after its extrema (the batch's candidate end and its raw /
-// record begins, lane-local), then four words per chain: work and done
-// counters of orientation and descriptor
+constexpr int kSlots = SIFT_MAX_INFLIGHT;
+// device counter block of a slot: [4L..4L+3] live counters of lane L
+// (candidates, refined, records), [8..11] zeros, then per keypoint batch g a
+// 4-word snapshot taken by the last extrema workgroup (the batch's candidate
+// end and its raw / record begins, lane-local; word 3 = that launch's done
+// counter), then four words per chain: work and done counters of
+// orientation and descriptor
 constexpr int kCtrZeros = 4 * kLanes;
 constexpr int kCtrSnap = kCtrZeros + 4;
 constexpr int kCtrWork = kCtrSnap + 4 * (kMaxOctaves + 1);
 constexpr int kCtrWords = kCtrWork + 4 * (kMaxOctaves + 2);
+// largest per-lane capacities (the kernels index with 32-bit unsigned)
+constexpr size_t kMaxCand = (size_t)1 << 28;
+constexpr size_t kMaxRec = (size_t)1 << 29;
 
 template <class T>
-struct Pinned {  // grow-only pinned host buffer (fast async D2H, no staging)
+struct Pinned {  // grow-only pinned host buffer (fast async copies, no staging)
     T* p = nullptr;
     size_t cap = 0;
     int ensure(size_t n) {
         if (p && cap >= n) return SIFT_OK;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         const size_t want = n < 1024 ? 1024 : n + n / 4;
-        if (hipHostMalloc(&p, want * sizeof(T)) != hipSuccess) return SIFT_ERR_NOMEM;
+        if (hipHostMalloc(&p, want * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            return SIFT_ERR_NOMEM;
+        }
         cap = want;
         return SIFT_OK;
     }
@@ -62,11 +79,6 @@ struct Pinned {  // grow-only pinned host buffer (fast async D2H, no staging)
         p = nullptr;
         cap = 0;
     }
-};
-
-struct Stage {
-    PyrTable pt;
-    BlurTaps taps[kMaxLevels];
 };
 
 // Grow-only mapped, coherent pinned host buffer: kernels write it directly
@@ -98,71 +110,121 @@ struct Mapped {
     }
 };
 
+template <class T>
+struct DevBuf {  // grow-only device buffer (contents not preserved)
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (p && cap >= n) return SIFT_OK;
+        release();
+        if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            return SIFT_ERR_NOMEM;
+        }
+        cap = n;
+        return SIFT_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Stage {
+    PyrTable pt;
+    BlurTaps taps[kMaxLevels];
+};
+
 struct EventPair {
     hipEvent_t a, b;
     double bytes;
+};
+
+enum SlotState { kFree = 0, kSubmitted = 1, kFinalized = 2 };
+
+// Everything one job owns; reused (grow-only) by later jobs in this slot.
+struct Slot {
+    int state = kFree;
+    int ticket = -1;
+    // the job
+    int n_img = 0, w = 0, h = 0, c = 0;
+    bool want_df = false;
+    sift_params p{};
+    Geometry g;
+    DevParams dp{};
+    BlurTaps taps_init{};
+    BlurTaps taps[kMaxLevels]{};
+    // device buffers
+    DevBuf<double> in;       // staged input images (doubles), contiguous
+    DevBuf<uint8_t> in8;     // staged input bytes (u8 upload path)
+    DevBuf<double> pyr;      // n_img pyramids of g.total doubles
+    DevBuf<double> tmp;      // generic wide-kernel blur temporaries
+    DevBuf<sift_extremum> cand;
+    DevBuf<RawKp> raw;
+    DevBuf<sift_kp> ori;
+    DevBuf<RecSide> side;
+    DevBuf<float> df32;
+    size_t cap_cand = 0, cap_raw = 0, cap_ori = 0;  // per lane
+    unsigned* d_ctr = nullptr;
+    unsigned* h_ctr = nullptr;  // pinned, live counters of every lane
+    Stage* h_stage = nullptr;
+    Stage* d_stage = nullptr;
+    PyrTable h_pt{};
+    Pinned<uint8_t> h_up;  // pinned upload staging
+    // records exported by k_descriptor per keypoint chain (mapped pinned)
+    Mapped<sift_kp> exp_rec;
+    Mapped<RecSide> exp_side;
+    Mapped<unsigned> exp_cnt;  // [begin, end) per chain
+    size_t exp_lane = 0;
+    std::vector<hipEvent_t> chain_ev, sync_ev, ev_pool;
+    std::vector<int> chain_lane;
+    int n_chains = 0, ev_i = 0;
+    size_t ev_used = 0;
+    hipEvent_t done_ev = nullptr;  // lane counters on the host
+    std::vector<EventPair> pending;
+    // finalize
+    bool exported = true;
+    unsigned n_lane[kLanes] = {};
+    unsigned lane_n[3][kLanes] = {};
+    size_t host_base[kLanes] = {};
+    const sift_kp* rec_src = nullptr;
+    std::vector<unsigned> keep, run_start;
+    std::vector<size_t> img_count;
+    size_t n_final = 0;
+    unsigned n_keys = 0;
+    FinalizeWorkspace fin_ws;
+    Pinned<sift_kp> h_ori;
+    Pinned<RecSide> h_side;
+    Pinned<float> h_df32;
+    sift_counts counts{};
+    clk::time_point t_submit;
+    double t_host[5] = {0, 0, 0, 0, 0};
 };
 
 }  // namespace
 
 struct sift_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;   // A: pyramid
+    hipStream_t stream = nullptr;   // A: pyramid (even octaves), public stream
     hipStream_t stream2 = nullptr;  // B: odd octaves of the pyramid
-    hipStream_t stream3 = nullptr;  // C: extrema, refine, orientation, descriptor
+    hipStream_t stream3 = nullptr;  // C: keypoint chains of even batches (lane 0)
     hipStream_t stream4 = nullptr;  // D: keypoint chains of odd batches (lane 1)
     // persistent workgroups of orientation / descriptor per launch: 512 (two
     // per CU; with two keypoint lanes in flight this leaves room for the
     // small octaves' blurs); measured best of 256/384/512/768/1024
     unsigned kp_wgs = 512;
-    int batch_px_log2 = 18;         // octaves of >= 2^this pixels get their own batch
-    std::vector<hipEvent_t> sync_ev;
+    int batch_px_log2 = 18;  // octaves of >= 2^this pixels (x images) get their own batch
+    int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
+    Slot slots[kSlots];
+    int next_ticket = 1;
+    int last = -1;  // slot of the last finalised job (introspection)
 
-    double* d_in = nullptr;
-    size_t in_cap = 0;  // elements
-    double* d_pyr = nullptr;
-    size_t pyr_cap = 0;
-    double* d_tmp = nullptr;
-    size_t tmp_cap = 0;
-
-    sift_extremum* d_cand = nullptr;
-    RawKp* d_raw = nullptr;
-    sift_kp* d_ori = nullptr;
-    double* d_off0 = nullptr;
-    float* d_df32 = nullptr;
-    // capacities per lane (each array holds kLanes regions of that size)
-    unsigned cap_cand = 0, cap_raw = 0, cap_ori = 0, cap_off0 = 0, cap_df32 = 0;
-    int lanes = kLanes;  // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
-    unsigned lane_n[3][kLanes] = {};  // last detect: candidates, refined, records per lane
-    unsigned* d_ctr = nullptr;
-    unsigned* h_ctr = nullptr;  // pinned, live counters of every lane
-    PyrTable h_pt{};
-    // per-call tables: pinned host staging -> one async copy -> device
-    Stage* h_stage = nullptr;
-    Stage* d_stage = nullptr;
-    PyrTable* d_pt = nullptr;     // &d_stage->pt
-    BlurTaps* d_taps = nullptr;   // d_stage->taps
-
-    // last detect
-    bool have_run = false;
-    sift_counts counts{};
-    sift_params last_p{};
-
-    // profiling
+    // profiling (pyramid kernels)
     bool profiling = false;
-    std::vector<hipEvent_t> ev_pool;
-    size_t ev_used = 0;
-    std::vector<EventPair> pending;
     double prof_ms = 0.0;
     int64_t prof_launches = 0;
     double prof_bytes = 0.0;
-
-    // records exported by k_descriptor per keypoint batch (mapped pinned)
-    Mapped<sift_kp> exp_rec;
-    Mapped<double> exp_off0;
-    Mapped<unsigned> exp_cnt;  // [begin, end) per chain
-    std::vector<hipEvent_t> chain_ev;
-    std::vector<unsigned> run_start;
 
     // matcher: one device arena (inputs, shifted rows, norms, results) and
     // pinned result staging
@@ -170,18 +232,6 @@ struct sift_ctx {
     size_t mbuf_cap = 0;
     Pinned<int> h_mj;
     Pinned<double> h_md;
-
-    // host staging (pinned)
-    Pinned<sift_kp> h_ori;
-    Pinned<double> h_off0;
-    Pinned<float> h_df32;
-    std::vector<unsigned> keep;
-    FinalizeWorkspace fin_ws;
-
-    // host-side phase wall times of the last detect (ms): enqueue, wait for
-    // the device pipeline, records download, finalize (size + sort/unique),
-    // output assembly
-    double t_host[5] = {0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -192,79 +242,34 @@ namespace {
         if (e_ != hipSuccess) return SIFT_ERR_HIP;  \
     } while (0)
 
-int ensure(double** p, size_t* cap, size_t need) {
-    if (*cap >= need) return SIFT_OK;
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    if (hipMalloc(p, need * sizeof(double)) != hipSuccess) return SIFT_ERR_NOMEM;
-    *cap = need;
-    return SIFT_OK;
-}
-
-template <class T>
-int ensure_t(T** p, unsigned* cap, unsigned need) {
-    if (*cap >= need && *p) return SIFT_OK;
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    if (hipMalloc(p, (size_t)need * sizeof(T)) != hipSuccess) return SIFT_ERR_NOMEM;
-    *cap = need;
-    return SIFT_OK;
-}
-
-// kLanes regions of `need` elements each; *cap = per-lane capacity
-template <class T>
-int ensure_lanes(T** p, unsigned* cap, unsigned need) {
-    if (*cap >= need && *p) return SIFT_OK;
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    if (hipMalloc(p, (size_t)need * kLanes * sizeof(T)) != hipSuccess) return SIFT_ERR_NOMEM;
-    *cap = need;
-    return SIFT_OK;
-}
-
-hipEvent_t next_event(sift_ctx* ctx) {
-    if (ctx->ev_used == ctx->ev_pool.size()) {
+hipEvent_t pool_event(Slot& s) {  // timing events (profiling)
+    if (s.ev_used == s.ev_pool.size()) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return nullptr;
-        ctx->ev_pool.push_back(e);
+        s.ev_pool.push_back(e);
     }
-    return ctx->ev_pool[ctx->ev_used++];
+    return s.ev_pool[s.ev_used++];
+}
+
+hipEvent_t sync_event(Slot& s) {  // untimed cross-stream events
+    while ((int)s.sync_ev.size() <= s.ev_i) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        s.sync_ev.push_back(e);
+    }
+    return s.sync_ev[s.ev_i++];
 }
 
 // Profiling events for one pyramid launch: timestamps recorded by the
 // dispatch packet itself (hipExtLaunchKernel), so timing adds no gaps.
-int prof_events(sift_ctx* ctx, hipEvent_t* e0, hipEvent_t* e1, double bytes) {
+int prof_events(sift_ctx* ctx, Slot& s, hipEvent_t* e0, hipEvent_t* e1, double bytes) {
     *e0 = *e1 = nullptr;
     if (!ctx->profiling) return SIFT_OK;
-    *e0 = next_event(ctx);
-    *e1 = next_event(ctx);
+    *e0 = pool_event(s);
+    *e1 = pool_event(s);
     if (!*e0 || !*e1) return SIFT_ERR_HIP;
-    ctx->pending.push_back({*e0, *e1, bytes});
+    s.pending.push_back({*e0, *e1, bytes});
     return SIFT_OK;
-}
-
-int blur_launch(sift_ctx* ctx, hipStream_t s, const double* src, double* dst, int W, int H,
-                const BlurTaps& t, double* dec, int Wd, int Hd) {
-    if (t.R > kMaxTemplR || t.R < 1) {
-        if (ensure(&ctx->d_tmp, &ctx->tmp_cap, (size_t)W * H) != SIFT_OK) return SIFT_ERR_NOMEM;
-    }
-    hipEvent_t e0, e1;
-    const double bytes = 16.0 * (double)W * (double)H + (dec ? 8.0 * (double)Wd * Hd : 0.0);
-    if (prof_events(ctx, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
-    SIFT_HIP_TRY(launch_blur(src, dst, W, H, t, dec, Wd, Hd, ctx->d_tmp, s, e0, e1));
-    return SIFT_OK;
-}
-
-hipEvent_t sync_event(sift_ctx* ctx, int i) {  // untimed cross-stream events
-    while ((int)ctx->sync_ev.size() <= i) {
-        hipEvent_t e;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-        ctx->sync_ev.push_back(e);
-    }
-    return ctx->sync_ev[i];
 }
 
 ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end) {
@@ -281,87 +286,180 @@ ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end) {
     return eg;
 }
 
-int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
-                const sift_params* p, sift_kp** out_kps, size_t* out_n,
-                float** out_desc_f32) {
-    using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
-    auto ms = [](clk::time_point a, clk::time_point b) {
-        return std::chrono::duration<double, std::milli>(b - a).count();
-    };
-    Geometry g;
-    BlurTaps taps_init;
-    std::vector<BlurTaps> taps(kMaxLevels);
-    DevParams dp;
-    int st = host_plan(p, w, h, c, &g, &taps_init, taps.data(), &dp);
-    if (st != SIFT_OK) return st;
-    SIFT_HIP_TRY(hipSetDevice(ctx->device));
-    ctx->have_run = false;
-    ctx->ev_used = 0;
-    ctx->pending.clear();
+// keypoint-array capacities of a slot (per lane), all size_t and bounded so
+// that the kernels' 32-bit indices and the df32 product never wrap
+int ensure_kp_arrays(Slot& s, size_t cand, size_t raw, size_t ori) {
+    if (cand > kMaxCand || raw > kMaxCand || ori > kMaxRec) return SIFT_ERR_NOMEM;
+    if (s.cand.ensure(cand * kLanes) != SIFT_OK) return SIFT_ERR_NOMEM;
+    if (s.raw.ensure(raw * kLanes) != SIFT_OK) return SIFT_ERR_NOMEM;
+    if (s.ori.ensure(ori * kLanes) != SIFT_OK) return SIFT_ERR_NOMEM;
+    if (s.side.ensure(ori * kLanes) != SIFT_OK) return SIFT_ERR_NOMEM;
+    if (s.want_df && s.df32.ensure(ori * kLanes * 128) != SIFT_OK) return SIFT_ERR_NOMEM;
+    s.cap_cand = cand;
+    s.cap_raw = raw;
+    s.cap_ori = ori;
+    return SIFT_OK;
+}
 
-    if ((st = ensure(&ctx->d_pyr, &ctx->pyr_cap, g.total)) != SIFT_OK) return st;
-    std::memset(&ctx->h_pt, 0, sizeof ctx->h_pt);
-    for (int o = 0; o < g.octaves; ++o) {
-        ctx->h_pt.w[o] = g.W[o];
-        ctx->h_pt.h[o] = g.H[o];
-        for (int l = 0; l < g.n_gauss; ++l) ctx->h_pt.lvl[o][l] = ctx->d_pyr + g.offs[o][l];
+// After a failure with work already enqueued: let every stream drain before
+// the slot's buffers can be touched again, then free the slot.
+void abandon(sift_ctx* ctx, Slot& s) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream2);
+    (void)hipStreamSynchronize(ctx->stream3);
+    (void)hipStreamSynchronize(ctx->stream4);
+    s.pending.clear();
+    s.state = kFree;
+    s.ticket = -1;
+}
+
+// ---------------------------------------------------------------------------
+// enqueue one job on slot s (everything up to the counter read-back)
+// ---------------------------------------------------------------------------
+int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
+    const auto t0 = clk::now();
+    s.t_submit = t0;
+    const Geometry& g = s.g;
+    const int n_img = s.n_img;
+    const sift_params* p = &s.p;
+    const DevParams& dp = s.dp;
+    s.ev_i = 0;
+    s.ev_used = 0;
+    s.pending.clear();
+    s.n_chains = 0;
+    s.chain_lane.clear();
+    int st;
+    hipStream_t sA = ctx->stream, sB = ctx->stream2, sC = ctx->stream3, sD = ctx->stream4;
+
+    // ---- input images -> device (contiguous, image b at src + b * in_bs)
+    const size_t ne = (size_t)s.w * s.h * s.c;
+    const double* src = nullptr;
+    const size_t in_bs = ne;
+    if (kind == SIFT_INPUT_F64_DEVICE && n_img == 1) {
+        src = static_cast<const double*>(images[0]);
+    } else {
+        if ((st = s.in.ensure(ne * n_img)) != SIFT_OK) return st;
+        src = s.in.p;
+        if (kind == SIFT_INPUT_F64_DEVICE) {
+            for (int b = 0; b < n_img; ++b)
+                SIFT_HIP_TRY(hipMemcpyAsync(s.in.p + b * ne, images[b], ne * sizeof(double),
+                                            hipMemcpyDeviceToDevice, sA));
+        } else if (kind == SIFT_INPUT_U8_DEVICE) {
+            for (int b = 0; b < n_img; ++b)
+                SIFT_HIP_TRY(launch_u8_to_f64(static_cast<const uint8_t*>(images[b]),
+                                              s.in.p + b * ne, ne, sA));
+        } else {
+            // host images through pinned staging: bytes when every value is an
+            // integer 0..255 (stb-decoded images always are; exact on the
+            // device), doubles otherwise
+            bool as_u8 = true;
+            if ((st = s.h_up.ensure(ne * n_img * sizeof(double))) != SIFT_OK) return st;
+            if (kind == SIFT_INPUT_U8_HOST) {
+                for (int b = 0; b < n_img; ++b)
+                    std::memcpy(s.h_up.p + b * ne, images[b], ne);
+            } else {
+                for (int b = 0; b < n_img && as_u8; ++b)
+                    as_u8 = host_pack_u8(static_cast<const double*>(images[b]), ne,
+                                         s.h_up.p + b * ne);
+                if (!as_u8)
+                    for (int b = 0; b < n_img; ++b)
+                        std::memcpy(s.h_up.p + b * ne * sizeof(double), images[b],
+                                    ne * sizeof(double));
+            }
+            if (as_u8) {
+                if ((st = s.in8.ensure(ne * n_img)) != SIFT_OK) return st;
+                SIFT_HIP_TRY(hipMemcpyAsync(s.in8.p, s.h_up.p, ne * n_img,
+                                            hipMemcpyHostToDevice, sA));
+                SIFT_HIP_TRY(launch_u8_to_f64(s.in8.p, s.in.p, ne * n_img, sA));
+            } else {
+                SIFT_HIP_TRY(hipMemcpyAsync(s.in.p, s.h_up.p, ne * n_img * sizeof(double),
+                                            hipMemcpyHostToDevice, sA));
+            }
+        }
     }
-    // the previous call's copy out of h_stage has completed (every detect
-    // ends with a stream synchronisation), so the staging can be rewritten
-    ctx->h_stage->pt = ctx->h_pt;
-    for (int l = 0; l < g.n_gauss; ++l) ctx->h_stage->taps[l] = taps[l];
-    SIFT_HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, sizeof(Stage),
-                                hipMemcpyHostToDevice, ctx->stream));
+
+    // ---- pyramid tables
+    const size_t stride = g.total;  // doubles per image pyramid
+    if ((st = s.pyr.ensure(stride * n_img)) != SIFT_OK) return st;
+    std::memset(&s.h_pt, 0, sizeof s.h_pt);
+    for (int o = 0; o < g.octaves; ++o) {
+        s.h_pt.w[o] = g.W[o];
+        s.h_pt.h[o] = g.H[o];
+        for (int l = 0; l < g.n_gauss; ++l) s.h_pt.lvl[o][l] = s.pyr.p + g.offs[o][l];
+    }
+    s.h_pt.img_stride = stride;
+    s.h_pt.n_img = n_img;
+    s.h_pt.n_oct = g.octaves;
+    // the slot's previous job has been fetched, so its copy out of h_stage
+    // has completed and the staging can be rewritten
+    s.h_stage->pt = s.h_pt;
+    for (int l = 0; l < g.n_gauss; ++l) s.h_stage->taps[l] = s.taps[l];
+    SIFT_HIP_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, sizeof(Stage), hipMemcpyHostToDevice, sA));
+    const PyrTable* d_pt = &s.d_stage->pt;
+
+    // wide kernels (R > kMaxTemplR) go through a temporary: one per pyramid
+    // stream parity (octaves o and o+1 overlap)
+    bool wide = s.taps_init.R > kMaxTemplR || s.taps_init.R < 1;
+    for (int l = 1; l < g.n_gauss; ++l) wide |= s.taps[l].R > kMaxTemplR || s.taps[l].R < 1;
+    const size_t tmp_half = (size_t)g.W[0] * g.H[0] * n_img;
+    if (wide && (st = s.tmp.ensure(2 * tmp_half)) != SIFT_OK) return st;
 
     // capacities for the variable-size stages; grown and re-run on overflow
-    unsigned want_cand = (unsigned)std::min<size_t>(std::max<size_t>(g.sum_px / 32, 65536),
-                                                   (size_t)1 << 28);
-    if ((st = ensure_lanes(&ctx->d_cand, &ctx->cap_cand, want_cand)) != SIFT_OK) return st;
-    if ((st = ensure_lanes(&ctx->d_raw, &ctx->cap_raw, ctx->cap_cand)) != SIFT_OK) return st;
-    if ((st = ensure_lanes(&ctx->d_ori, &ctx->cap_ori, 2 * ctx->cap_raw)) != SIFT_OK) return st;
-    if ((st = ensure_lanes(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
-    if (out_desc_f32 &&
-        (st = ensure_lanes(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
+    const size_t want_cand =
+        std::min<size_t>(std::max<size_t>(g.sum_px * n_img / 32, 65536), kMaxCand);
+    if ((st = ensure_kp_arrays(s, std::max(s.cap_cand, want_cand),
+                               std::max(s.cap_raw, want_cand),
+                               std::max(s.cap_ori, 2 * want_cand))) != SIFT_OK)
         return st;
 
-    // Three streams (HIP's default is four hardware queues per process, and
-    // streams beyond that share a queue and serialise): A (ctx->stream) and
-    // B (ctx->stream2) build the pyramid, even and odd octaves, at high
-    // priority; C (ctx->stream3) runs, per octave batch as soon as its levels
-    // exist, the extrema then refine -> orientation -> descriptor. The
-    // keypoint work of octave 0 overlaps the pyramid of the smaller octaves,
-    // which is latency-bound and leaves most of the chip idle.
-    hipStream_t sA = ctx->stream, sB = ctx->stream2, sC = ctx->stream3, sD = ctx->stream4;
     const int lanes = ctx->lanes;
     hipStream_t lane_stream[kLanes] = {sC, sD};
-    int ev_i = 0;
+    SIFT_HIP_TRY(hipMemsetAsync(s.d_ctr, 0, kCtrWords * sizeof(unsigned), sA));
 
-    SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sA));
+    auto blur = [&](hipStream_t so, int o, int l, const double* bsrc, size_t src_bs,
+                    const BlurTaps& t, bool dec) -> int {
+        const int W = g.W[o], H = g.H[o];
+        const int Wd = dec ? g.W[o + 1] : 0, Hd = dec ? g.H[o + 1] : 0;
+        hipEvent_t e0, e1;
+        const double bytes =
+            n_img * (16.0 * (double)W * (double)H + (dec ? 8.0 * (double)Wd * Hd : 0.0));
+        if (prof_events(ctx, s, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
+        double* dst = s.h_pt.lvl[o][l];
+        double* decp = dec ? s.h_pt.lvl[o + 1][0] : nullptr;
+        double* tmp = wide ? s.tmp.p + (o & 1) * tmp_half : nullptr;
+        SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp, so,
+                                 e0, e1));
+        return SIFT_OK;
+    };
+
     // ---- Gaussian pyramid (compute_initial_image + compute_gaussian_images)
     const int W0 = g.W[0], H0 = g.H[0];
-    double* G00 = ctx->h_pt.lvl[0][0];
     {
         hipEvent_t e0, e1;
-        if (prof_events(ctx, &e0, &e1, 16.0 * (double)W0 * H0) != SIFT_OK) return SIFT_ERR_HIP;
+        if (prof_events(ctx, s, &e0, &e1, 16.0 * n_img * (double)W0 * H0) != SIFT_OK)
+            return SIFT_ERR_HIP;
         hipError_t err = hipSuccess;
-        const bool fused = launch_blur_initial_fused(d_img, w, h, c, p->double_image_size ? 1 : 0,
-                                                     G00, W0, H0, taps_init, sA, e0, e1, &err);
+        const bool fused = launch_blur_initial_fused(src, in_bs, s.w, s.h, s.c,
+                                                     p->double_image_size ? 1 : 0,
+                                                     s.h_pt.lvl[0][0], stride, n_img, W0, H0,
+                                                     s.taps_init, sA, e0, e1, &err);
         if (fused) {
             SIFT_HIP_TRY(err);
         } else {
-            if (ctx->profiling) ctx->pending.pop_back();
-            const double* base_src = d_img;
-            if (c != 1 || p->double_image_size) {
+            if (ctx->profiling) s.pending.pop_back();
+            const double* base_src = src;
+            size_t base_bs = in_bs;
+            if (s.c != 1 || p->double_image_size) {
                 // gray (+ bilinear x2) into level 1's storage; level 1 is
                 // written by the first octave blur, after G[0][0] exists
-                double* scratch = ctx->h_pt.lvl[0][1];
-                SIFT_HIP_TRY(launch_prepare(d_img, w, h, c, p->double_image_size ? 1 : 0,
-                                            scratch, W0, H0, sA));
+                double* scratch = s.h_pt.lvl[0][1];
+                SIFT_HIP_TRY(launch_prepare(src, in_bs, s.w, s.h, s.c,
+                                            p->double_image_size ? 1 : 0, scratch, stride, W0,
+                                            H0, n_img, sA));
                 base_src = scratch;
+                base_bs = stride;
             }
-            if ((st = blur_launch(ctx, sA, base_src, G00, W0, H0, taps_init, nullptr, 0, 0)) !=
-                SIFT_OK)
+            if ((st = blur(sA, 0, 0, base_src, base_bs, s.taps_init, false)) != SIFT_OK)
                 return st;
         }
     }
@@ -375,97 +473,91 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
             break;
         }
     const bool tiles = p->window_size / 2 == 1;
-    // Keypoint batches on stream C: each large octave (>= batch_px pixels) is
-    // its own batch as soon as its levels exist; the smaller ones, whose
-    // keypoint work is too small to amortise a chain of launches, form one
-    // final batch. A batch: extrema, a counter snapshot (its candidate end,
-    // raw / record begins), refine, orientation, descriptor.
+    // Keypoint batches: each large octave (>= batch_px pixels over the job's
+    // images) is its own batch as soon as its levels exist; the smaller ones,
+    // whose keypoint work is too small to amortise a chain of launches, form
+    // one final batch. The final batch starts no later than o_small: octaves
+    // built by k_octaves_lds have no per-octave batch of their own.
     const size_t batch_px = (size_t)1 << ctx->batch_px_log2;
     int o_merge = g.octaves;  // first octave of the final batch
     for (int o = 0; o < g.octaves; ++o)
-        if ((size_t)g.W[o] * g.H[o] < batch_px) {
+        if ((size_t)g.W[o] * g.H[o] * n_img < batch_px) {
             o_merge = o;
             break;
         }
-    const unsigned* zeros = ctx->d_ctr + kCtrZeros;
-    auto snap = [&](int g) { return ctx->d_ctr + kCtrSnap + 4 * g; };
-    auto launch_extrema_range = [&](int o_begin, int o_end, int L) -> int {
-        hipStream_t sx = lane_stream[L];
-        sift_extremum* cand = ctx->d_cand + (size_t)L * ctx->cap_cand;
-        unsigned* live = ctx->d_ctr + 4 * L;
-        if (tiles) {
-            const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
-            SIFT_HIP_TRY(launch_extrema_tiles(ctx->d_pt, eg, g.n_gauss, dp.threshold, cand,
-                                              live + 0, ctx->cap_cand, sx));
-        } else {
-            for (int o = o_begin; o < o_end; ++o)
-                SIFT_HIP_TRY(launch_extrema_any(ctx->d_pt, o, g.W[o], g.H[o], g.n_gauss,
-                                                p->window_size, dp.threshold, cand, live + 0,
-                                                ctx->cap_cand, sx));
-        }
-        return SIFT_OK;
-    };
+    o_merge = std::min(o_merge, o_small);
+    const unsigned* zeros = s.d_ctr + kCtrZeros;
+    auto snap = [&](int gb) { return s.d_ctr + kCtrSnap + 4 * gb; };
     // records of every chain also go to the mapped export buffers, sized from
     // the largest record count seen so far (a larger one falls back to one
     // bulk download at the end, and grows them for the next call)
-    if ((st = ctx->exp_rec.ensure(std::max<size_t>(ctx->exp_rec.cap, 16384 * kLanes))) !=
-            SIFT_OK ||
-        (st = ctx->exp_off0.ensure(ctx->exp_rec.cap)) != SIFT_OK ||
-        (st = ctx->exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
+    const size_t exp_want = std::max<size_t>(s.exp_rec.cap, (size_t)8192 * n_img * kLanes);
+    if ((st = s.exp_rec.ensure(exp_want)) != SIFT_OK ||
+        (st = s.exp_side.ensure(s.exp_rec.cap)) != SIFT_OK ||
+        (st = s.exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
         return st;
     // poison: a range no launch published reads as "not exported"
-    std::fill(ctx->exp_cnt.h, ctx->exp_cnt.h + ctx->exp_cnt.cap, 0xFFFFFFFFu);
+    std::fill(s.exp_cnt.h, s.exp_cnt.h + s.exp_cnt.cap, 0xFFFFFFFFu);
     // lane L exports its records (lane-local index i) to exp_rec[L * exp_lane + i]
-    const unsigned exp_lane = (unsigned)(ctx->exp_rec.cap / kLanes);
-    int n_chains = 0;
-    std::vector<int> chain_lane;
+    s.exp_lane = s.exp_rec.cap / kLanes;
+
     // extrema over [o_begin, o_end) then refine -> orientation -> descriptor,
-    // on lane L. `begin` (a counter snapshot taken right after the extrema)
-    // holds this batch's candidate end and its raw / record begins; candidates
-    // start at cand_begin (the lane's previous batch's snapshot). The re-run
-    // passes nullptr (lane 0, live counters).
+    // on lane L. `begin` (the snapshot written by the extrema launch's last
+    // workgroup) holds this batch's candidate end and its raw / record
+    // begins; candidates start at cand_begin (the lane's previous batch's
+    // snapshot). The overflow re-run passes nullptr (lane 0, live counters).
+    const unsigned cap_cand = (unsigned)s.cap_cand, cap_raw = (unsigned)s.cap_raw,
+                   cap_ori = (unsigned)s.cap_ori;
     auto run_chain = [&](int L, int o_begin, int o_end, const unsigned* cand_begin,
                          unsigned* begin) -> int {
-        const int ci = n_chains++;
-        chain_lane.push_back(L);
+        const int ci = s.n_chains++;
+        s.chain_lane.push_back(L);
         hipStream_t sx = lane_stream[L];
-        unsigned* live = ctx->d_ctr + 4 * L;
-        sift_extremum* cand = ctx->d_cand + (size_t)L * ctx->cap_cand;
-        RawKp* raw = ctx->d_raw + (size_t)L * ctx->cap_raw;
-        sift_kp* recs = ctx->d_ori + (size_t)L * ctx->cap_ori;
-        double* off0 = ctx->d_off0 + (size_t)L * ctx->cap_ori;
-        float* df32 = out_desc_f32 ? ctx->d_df32 + (size_t)L * ctx->cap_ori * 128 : nullptr;
-        unsigned* work = ctx->d_ctr + kCtrWork + 4 * ci;
-        while ((int)ctx->chain_ev.size() <= ci) {
+        unsigned* live = s.d_ctr + 4 * L;
+        sift_extremum* cand = s.cand.p + (size_t)L * s.cap_cand;
+        RawKp* raw = s.raw.p + (size_t)L * s.cap_raw;
+        sift_kp* recs = s.ori.p + (size_t)L * s.cap_ori;
+        RecSide* side = s.side.p + (size_t)L * s.cap_ori;
+        float* df32 = s.want_df ? s.df32.p + (size_t)L * s.cap_ori * 128 : nullptr;
+        unsigned* work = s.d_ctr + kCtrWork + 4 * ci;
+        while ((int)s.chain_ev.size() <= ci) {
             hipEvent_t e;
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
                 return SIFT_ERR_HIP;
-            ctx->chain_ev.push_back(e);
+            s.chain_ev.push_back(e);
         }
-        const ExportSink ex{ctx->exp_rec.d + (size_t)L * exp_lane,
-                            ctx->exp_off0.d + (size_t)L * exp_lane, ctx->exp_cnt.d + 2 * ci,
-                            exp_lane};
-        int st2 = launch_extrema_range(o_begin, o_end, L);
-        if (st2 != SIFT_OK) return st2;
-        if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 4));
+        const ExportSink ex{s.exp_rec.d + (size_t)L * s.exp_lane,
+                            s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
+                            (unsigned)s.exp_lane};
+        if (tiles) {
+            const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
+            SIFT_HIP_TRY(launch_extrema_tiles(d_pt, eg, n_img, g.n_gauss, dp.threshold, cand,
+                                              live + 0, cap_cand, begin, sx));
+        } else {
+            for (int o = o_begin; o < o_end; ++o)
+                SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], n_img, g.n_gauss,
+                                                p->window_size, dp.threshold, cand, live + 0,
+                                                cap_cand, sx));
+            if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 3));
+        }
         const unsigned* b = begin ? begin : zeros;
-        SIFT_HIP_TRY(launch_refine(ctx->d_pt, dp, cand, cand_begin, begin ? begin : live + 0,
-                                   ctx->cap_cand, raw, live + 1, ctx->cap_raw, sx));
-        SIFT_HIP_TRY(launch_orient(ctx->d_pt, dp, raw, b + 1, live + 1, ctx->cap_raw, recs, off0,
-                                   live + 2, ctx->cap_ori, work, ctx->kp_wgs, sx));
-        SIFT_HIP_TRY(launch_descriptor(ctx->d_pt, dp, recs, off0, b + 2, live + 2, ctx->cap_ori,
-                                       df32, work + 2, ex, ctx->kp_wgs, sx));
-        SIFT_HIP_TRY(hipEventRecord(ctx->chain_ev[ci], sx));
+        SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
+                                   raw, live + 1, cap_raw, sx));
+        SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
+                                   cap_ori, work, ctx->kp_wgs, sx));
+        SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
+                                       work + 2, ex, ctx->kp_wgs, sx));
+        SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], sx));
         return SIFT_OK;
     };
     int n_batches = 0;
-    // batch g (lane g % lanes): octaves [o_begin, o_end), whose levels were
-    // enqueued on `sps`
+    // batch gb (lane gb % lanes): octaves [o_begin, o_end), whose levels
+    // were enqueued on `sps`
     auto batch = [&](int o_begin, int o_end, std::initializer_list<hipStream_t> sps) -> int {
         const int gb = n_batches++;
         const int L = gb % lanes;
         for (hipStream_t sp : sps) {
-            hipEvent_t pyr_done = sync_event(ctx, ev_i++);
+            hipEvent_t pyr_done = sync_event(s);
             if (!pyr_done) return SIFT_ERR_HIP;
             SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
             SIFT_HIP_TRY(hipStreamWaitEvent(lane_stream[L], pyr_done, 0));
@@ -478,224 +570,313 @@ int detect_impl(sift_ctx* ctx, const double* d_img, int w, int h, int c,
     // octave o (the small octaves are latency-bound: two in flight at once).
     hipStream_t pyr[2] = {sA, sB};
     hipEvent_t base_ready = nullptr;  // next octave's base written (decimation)
-    auto next_base_event = [&](hipStream_t so) -> int {
-        base_ready = sync_event(ctx, ev_i++);
+    if (o_small > 0 || o_small < g.octaves) {
+        // stream B's first octave must also see the input staging on A
+        base_ready = sync_event(s);
         if (!base_ready) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(base_ready, so));
-        return SIFT_OK;
-    };
+        SIFT_HIP_TRY(hipEventRecord(base_ready, sA));
+    }
     for (int o = 0; o < o_small; ++o) {
         hipStream_t so = pyr[o & 1];
         if (o > 0) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
         for (int l = 1; l < g.n_gauss; ++l) {
             const bool dec = (l == dec_level) && (o + 1 < g.octaves);
-            st = blur_launch(ctx, so, ctx->h_pt.lvl[o][l - 1], ctx->h_pt.lvl[o][l], g.W[o],
-                             g.H[o], taps[l], dec ? ctx->h_pt.lvl[o + 1][0] : nullptr,
-                             dec ? g.W[o + 1] : 0, dec ? g.H[o + 1] : 0);
-            if (st != SIFT_OK) return st;
-            if (dec && (st = next_base_event(so)) != SIFT_OK) return st;
+            if ((st = blur(so, o, l, s.h_pt.lvl[o][l - 1], stride, s.taps[l], dec)) != SIFT_OK)
+                return st;
+            if (dec) {
+                base_ready = sync_event(s);
+                if (!base_ready) return SIFT_ERR_HIP;
+                SIFT_HIP_TRY(hipEventRecord(base_ready, so));
+            }
         }
         if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
     }
     if (o_small < g.octaves) {
         hipStream_t so = pyr[o_small & 1];
-        if (o_small > 0) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
+        SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
         double bytes = 0.0;
         for (int o = o_small; o < g.octaves; ++o) {
             bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[o] * (double)g.H[o];
             if (o + 1 < g.octaves) bytes += 8.0 * (double)g.W[o + 1] * (double)g.H[o + 1];
         }
         hipEvent_t e0, e1;
-        if (prof_events(ctx, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(launch_octaves_lds(ctx->d_pt, o_small, g.octaves - 1, g.n_gauss,
-                                        ctx->d_taps, so, e0, e1));
+        if (prof_events(ctx, s, &e0, &e1, bytes * n_img) != SIFT_OK) return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss, s.d_stage->taps,
+                                        n_img, so, e0, e1));
     }
     if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
-    // stream B joins A (the ctx's public stream) before the call returns, and
-    // lane D joins C (the counters are read back on C)
+    // lane D joins C, then the live counters come back on C: the job's last
+    // device work (the final batch waited on both pyramid streams)
     {
-        hipEvent_t j = sync_event(ctx, ev_i++);
-        if (!j) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(j, sB));
-        SIFT_HIP_TRY(hipStreamWaitEvent(sA, j, 0));
-        hipEvent_t jd = sync_event(ctx, ev_i++);
+        hipEvent_t jd = sync_event(s);
         if (!jd) return SIFT_ERR_HIP;
         SIFT_HIP_TRY(hipEventRecord(jd, sD));
         SIFT_HIP_TRY(hipStreamWaitEvent(sC, jd, 0));
     }
-
-    // ---- finalise each batch on the host while the device runs the next:
-    // sizes with glibc pow and a sorted run per batch, from the exported
-    // records (sift.cpp:20-24, 427-429)
-    SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * kLanes * sizeof(unsigned),
+    SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                 hipMemcpyDeviceToHost, sC));
-    clk::time_point t_enq = clk::now(), t_wait;
-    bool exported = true;
-    unsigned n_keys = 0;
-    ctx->run_start.clear();
-    ctx->fin_ws.all.resize(ctx->exp_rec.cap);
-    for (int ci = 0; ci < n_chains; ++ci) {
-        SIFT_HIP_TRY(hipEventSynchronize(ctx->chain_ev[ci]));
-        const unsigned b = ctx->exp_cnt.h[2 * ci], e = ctx->exp_cnt.h[2 * ci + 1];
-        if (e > exp_lane || b > e) {
-            exported = false;
+    SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
+    s.t_host[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return SIFT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// finalise a submitted job on the host: per-chain sizes + sorted runs as the
+// chains complete, overflow re-run, merge + unique per image
+// ---------------------------------------------------------------------------
+int finalize_job(sift_ctx* ctx, Slot& s) {
+    const auto t0 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const Geometry& g = s.g;
+    const sift_params* p = &s.p;
+    int st;
+    hipStream_t sC = ctx->stream3;
+    s.exported = true;
+    s.n_keys = 0;
+    s.run_start.clear();
+    s.fin_ws.all.resize(s.exp_rec.cap);
+    for (int ci = 0; ci < s.n_chains; ++ci) {
+        SIFT_HIP_TRY(hipEventSynchronize(s.chain_ev[ci]));
+        const unsigned b = s.exp_cnt.h[2 * ci], e = s.exp_cnt.h[2 * ci + 1];
+        if (e > s.exp_lane || b > e) {
+            s.exported = false;
             break;
         }
-        const unsigned base = (unsigned)chain_lane[ci] * exp_lane;
-        host_sizes(p, ctx->exp_rec.h, ctx->exp_off0.h, base + b, base + e);
-        ctx->run_start.push_back(n_keys);
-        host_sort_run(ctx->exp_rec.h, base + b, base + e, ctx->fin_ws.all.data() + n_keys,
-                      &ctx->fin_ws);
-        n_keys += e - b;
+        const size_t base = (size_t)s.chain_lane[ci] * s.exp_lane;
+        host_sizes(p, s.exp_rec.h, s.exp_side.h, base + b, base + e);
+        s.run_start.push_back(s.n_keys);
+        host_sort_run(s.exp_rec.h, s.exp_side.h, (unsigned)(base + b), (unsigned)(base + e),
+                      s.fin_ws.all.data() + s.n_keys, &s.fin_ws);
+        s.n_keys += e - b;
     }
-    ctx->run_start.push_back(n_keys);
+    s.run_start.push_back(s.n_keys);
 
     // ---- the counters; re-run every candidate stage on overflow
+    clk::time_point t_wait;
     for (int attempt = 0;; ++attempt) {
-        if (attempt > 0) {  // pyramid is complete; one batch over everything, on C
-            exported = false;
-            SIFT_HIP_TRY(hipMemsetAsync(ctx->d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
-            SIFT_HIP_TRY(hipStreamSynchronize(sC));
-            n_chains = 0;
-            chain_lane.clear();
-            if ((st = run_chain(0, 0, g.octaves, zeros, nullptr)) != SIFT_OK) return st;
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ctr, ctx->d_ctr, 4 * kLanes * sizeof(unsigned),
+        if (attempt > 0) {
+            // the pyramid is complete: one chain over every octave, on C.
+            // Later jobs may be queued on the streams; they use other slots'
+            // buffers, and the re-run simply queues behind them.
+            s.exported = false;
+            SIFT_HIP_TRY(hipMemsetAsync(s.d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
+            s.n_chains = 0;
+            s.chain_lane.clear();
+            // re-enqueue through the same code path with a single chain
+            const bool tiles = p->window_size / 2 == 1;
+            const PyrTable* d_pt = &s.d_stage->pt;
+            unsigned* live = s.d_ctr;
+            const unsigned* zeros = s.d_ctr + kCtrZeros;
+            unsigned* work = s.d_ctr + kCtrWork;
+            const unsigned cap_cand = (unsigned)s.cap_cand, cap_raw = (unsigned)s.cap_raw,
+                           cap_ori = (unsigned)s.cap_ori;
+            const ExportSink ex{s.exp_rec.d, s.exp_side.d, nullptr, 0};
+            if (tiles) {
+                const ExtremaGrid eg = extrema_grid(g, 0, g.octaves);
+                SIFT_HIP_TRY(launch_extrema_tiles(d_pt, eg, s.n_img, g.n_gauss, s.dp.threshold,
+                                                  s.cand.p, live, cap_cand, nullptr, sC));
+            } else {
+                for (int o = 0; o < g.octaves; ++o)
+                    SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], s.n_img, g.n_gauss,
+                                                    p->window_size, s.dp.threshold, s.cand.p,
+                                                    live, cap_cand, sC));
+            }
+            SIFT_HIP_TRY(launch_refine(d_pt, s.dp, s.cand.p, zeros, live, cap_cand, s.raw.p,
+                                       live + 1, cap_raw, sC));
+            SIFT_HIP_TRY(launch_orient(d_pt, s.dp, s.raw.p, zeros, live + 1, cap_raw, s.ori.p,
+                                       s.side.p, live + 2, cap_ori, work, ctx->kp_wgs, sC));
+            SIFT_HIP_TRY(launch_descriptor(d_pt, s.dp, s.ori.p, s.side.p, zeros, live + 2, cap_ori,
+                                           s.want_df ? s.df32.p : nullptr, work + 2, ex,
+                                           ctx->kp_wgs, sC));
+            SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
+            SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
         }
-        SIFT_HIP_TRY(hipStreamSynchronize(sC));
+        SIFT_HIP_TRY(hipEventSynchronize(s.done_ev));
         t_wait = clk::now();
-        unsigned nc = 0, nr = 0, no = 0;  // largest per-lane counts
+        size_t nc = 0, nr = 0, no = 0;  // largest per-lane counts
         for (int L = 0; L < kLanes; ++L) {
-            nc = std::max(nc, ctx->h_ctr[4 * L]);
-            nr = std::max(nr, ctx->h_ctr[4 * L + 1]);
-            no = std::max(no, ctx->h_ctr[4 * L + 2]);
+            nc = std::max<size_t>(nc, s.h_ctr[4 * L]);
+            nr = std::max<size_t>(nr, s.h_ctr[4 * L + 1]);
+            no = std::max<size_t>(no, s.h_ctr[4 * L + 2]);
         }
-        if (nc <= ctx->cap_cand && nr <= ctx->cap_raw && no <= ctx->cap_ori) break;
+        if (nc <= s.cap_cand && nr <= s.cap_raw && no <= s.cap_ori) break;
         if (attempt >= 3) return SIFT_ERR_NOMEM;
         // grow every stage that overflowed (refine/orient counts are lower
-        // bounds when an upstream stage overflowed, so grow generously)
-        const unsigned nc2 = std::max(ctx->cap_cand, nc) * 2u;
-        const unsigned nr2 = std::max(std::max(ctx->cap_raw, nr) * 2u, nc2);
-        const unsigned no2 = std::max(std::max(ctx->cap_ori, no) * 2u, 2u * nr2);
-        if ((st = ensure_lanes(&ctx->d_cand, &ctx->cap_cand, nc2)) != SIFT_OK) return st;
-        if ((st = ensure_lanes(&ctx->d_raw, &ctx->cap_raw, nr2)) != SIFT_OK) return st;
-        if ((st = ensure_lanes(&ctx->d_ori, &ctx->cap_ori, no2)) != SIFT_OK) return st;
-        if ((st = ensure_lanes(&ctx->d_off0, &ctx->cap_off0, ctx->cap_ori)) != SIFT_OK) return st;
-        if (out_desc_f32 &&
-            (st = ensure_lanes(&ctx->d_df32, &ctx->cap_df32, ctx->cap_ori * 128u)) != SIFT_OK)
-            return st;
+        // bounds when an upstream stage overflowed, so grow generously);
+        // ensure_kp_arrays rejects capacities the kernels cannot index
+        const size_t nc2 = std::max(s.cap_cand, nc) * 2;
+        const size_t nr2 = std::max(std::max(s.cap_raw, nr) * 2, nc2);
+        const size_t no2 = std::max(std::max(s.cap_ori, no) * 2, 2 * nr2);
+        if ((st = ensure_kp_arrays(s, nc2, nr2, no2)) != SIFT_OK) return st;
     }
 
-    unsigned n_lane[kLanes];  // records per lane
     unsigned n_ori = 0;
     for (int L = 0; L < kLanes; ++L) {
-        n_lane[L] = ctx->h_ctr[4 * L + 2];
-        ctx->lane_n[0][L] = ctx->h_ctr[4 * L];
-        ctx->lane_n[1][L] = ctx->h_ctr[4 * L + 1];
-        ctx->lane_n[2][L] = n_lane[L];
-        n_ori += n_lane[L];
+        s.n_lane[L] = s.h_ctr[4 * L + 2];
+        s.lane_n[0][L] = s.h_ctr[4 * L];
+        s.lane_n[1][L] = s.h_ctr[4 * L + 1];
+        s.lane_n[2][L] = s.n_lane[L];
+        n_ori += s.n_lane[L];
     }
-    if (exported && n_keys != n_ori) exported = false;
-    const sift_kp* rec_src = ctx->exp_rec.h;
+    if (s.exported && s.n_keys != n_ori) s.exported = false;
+    s.rec_src = s.exp_rec.h;
     // host position of lane L's record i: exported, L * exp_lane + i; after a
     // bulk download, the lanes are concatenated
-    size_t host_base[kLanes];
-    for (int L = 0, acc = 0; L < kLanes; acc += n_lane[L], ++L)
-        host_base[L] = exported ? (size_t)L * exp_lane : (size_t)acc;
-    if (!exported) {  // bulk download of every record
-        if ((st = ctx->h_ori.ensure(n_ori)) != SIFT_OK) return st;
-        if ((st = ctx->h_off0.ensure(n_ori)) != SIFT_OK) return st;
+    const RecSide* side_src = s.exp_side.h;
+    for (int L = 0, acc = 0; L < kLanes; acc += s.n_lane[L], ++L)
+        s.host_base[L] = s.exported ? (size_t)L * s.exp_lane : (size_t)acc;
+    const bool bulk = !s.exported;
+    if (bulk) {  // bulk download of every record
+        if ((st = s.h_ori.ensure(n_ori)) != SIFT_OK) return st;
+        if ((st = s.h_side.ensure(n_ori)) != SIFT_OK) return st;
         for (int L = 0; L < kLanes; ++L) {
-            if (!n_lane[L]) continue;
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_ori.p + host_base[L],
-                                        ctx->d_ori + (size_t)L * ctx->cap_ori,
-                                        n_lane[L] * sizeof(sift_kp), hipMemcpyDeviceToHost, sC));
-            SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_off0.p + host_base[L],
-                                        ctx->d_off0 + (size_t)L * ctx->cap_ori,
-                                        n_lane[L] * sizeof(double), hipMemcpyDeviceToHost, sC));
+            if (!s.n_lane[L]) continue;
+            SIFT_HIP_TRY(hipMemcpyAsync(s.h_ori.p + s.host_base[L], s.ori.p + (size_t)L * s.cap_ori,
+                                        s.n_lane[L] * sizeof(sift_kp), hipMemcpyDeviceToHost, sC));
+            SIFT_HIP_TRY(hipMemcpyAsync(s.h_side.p + s.host_base[L],
+                                        s.side.p + (size_t)L * s.cap_ori,
+                                        s.n_lane[L] * sizeof(RecSide), hipMemcpyDeviceToHost, sC));
         }
-        rec_src = ctx->h_ori.p;
+        s.rec_src = s.h_ori.p;
+        side_src = s.h_side.p;
     }
-    if (out_desc_f32) {
-        const size_t span = exported ? ctx->exp_rec.cap : (size_t)n_ori;
-        if ((st = ctx->h_df32.ensure(std::max<size_t>(span, 1) * 128)) != SIFT_OK) return st;
+    if (s.want_df) {
+        const size_t span = s.exported ? s.exp_rec.cap : (size_t)n_ori;
+        if ((st = s.h_df32.ensure(std::max<size_t>(span, 1) * 128)) != SIFT_OK) return st;
         for (int L = 0; L < kLanes; ++L)
-            if (n_lane[L])
-                SIFT_HIP_TRY(hipMemcpyAsync(ctx->h_df32.p + host_base[L] * 128,
-                                            ctx->d_df32 + (size_t)L * ctx->cap_ori * 128,
-                                            (size_t)n_lane[L] * 128 * sizeof(float),
+            if (s.n_lane[L])
+                SIFT_HIP_TRY(hipMemcpyAsync(s.h_df32.p + s.host_base[L] * 128,
+                                            s.df32.p + (size_t)L * s.cap_ori * 128,
+                                            (size_t)s.n_lane[L] * 128 * sizeof(float),
                                             hipMemcpyDeviceToHost, sC));
     }
-    SIFT_HIP_TRY(hipStreamSynchronize(sC));
+    if (bulk || s.want_df) {
+        SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
+        SIFT_HIP_TRY(hipEventSynchronize(s.done_ev));
+    }
     const auto t_copy = clk::now();
 
     if (ctx->profiling) {
-        for (const EventPair& e : ctx->pending) {
+        for (const EventPair& e : s.pending) {
             float ems = 0.f;
             SIFT_HIP_TRY(hipEventElapsedTime(&ems, e.a, e.b));
             ctx->prof_ms += ems;
             ctx->prof_bytes += e.bytes;
             ctx->prof_launches += 1;
         }
-        ctx->pending.clear();
     }
+    s.pending.clear();
 
-    // clean_keypoints: merge the sorted runs and unique (or all of it, after
-    // a bulk download), in the g++-built layer
-    ctx->keep.resize(std::max<unsigned>(n_ori, 1));
-    size_t n;
-    if (exported) {
-        n = host_merge_unique(ctx->exp_rec.h, ctx->fin_ws.all.data(), ctx->run_start,
-                              ctx->keep.data(), &ctx->fin_ws);
+    // clean_keypoints per image: merge the sorted runs and unique (or all of
+    // it, after a bulk download), in the g++-built layer
+    s.keep.resize(std::max<unsigned>(n_ori, 1));
+    s.img_count.assign(s.n_img, 0);
+    if (s.exported) {
+        s.n_final = host_merge_unique(s.fin_ws.all.data(), s.run_start, s.keep.data(),
+                                      s.img_count.data(), &s.fin_ws);
     } else {
-        n = host_finalize(p, ctx->h_ori.p, ctx->h_off0.p, n_ori, ctx->keep.data(),
-                          &ctx->fin_ws);
-        // the next call exports this many records per lane
-        const unsigned lane_max = std::max(n_lane[0], n_lane[1]);
-        if (lane_max > exp_lane) {
+        s.n_final = host_finalize(p, s.h_ori.p, side_src, n_ori, s.keep.data(),
+                                  s.img_count.data(), &s.fin_ws);
+        // the next job in this slot exports this many records per lane
+        const unsigned lane_max = std::max(s.n_lane[0], s.n_lane[1]);
+        if (lane_max > s.exp_lane) {
             const size_t want = ((size_t)lane_max + lane_max / 2) * kLanes;
-            if ((st = ctx->exp_rec.ensure(want)) != SIFT_OK ||
-                (st = ctx->exp_off0.ensure(want)) != SIFT_OK)
+            if ((st = s.exp_rec.ensure(want)) != SIFT_OK ||
+                (st = s.exp_side.ensure(want)) != SIFT_OK)
                 return st;
         }
     }
     const auto t_fin = clk::now();
+    s.t_host[1] = ms(t0, t_wait);
+    s.t_host[2] = ms(t_wait, t_copy);
+    s.t_host[3] = ms(t_copy, t_fin);
 
-    sift_kp* kps = (sift_kp*)std::malloc(std::max<size_t>(n, 1) * sizeof(sift_kp));
-    if (!kps) return SIFT_ERR_NOMEM;
-    for (size_t i = 0; i < n; ++i) kps[i] = rec_src[ctx->keep[i]];
-    float* df = nullptr;
-    if (out_desc_f32) {
-        df = (float*)std::malloc(std::max<size_t>(n, 1) * 128 * sizeof(float));
-        if (!df) {
-            std::free(kps);
-            return SIFT_ERR_NOMEM;
-        }
-        for (size_t i = 0; i < n; ++i)
-            std::memcpy(df + i * 128, ctx->h_df32.p + (size_t)ctx->keep[i] * 128,
-                        128 * sizeof(float));
-    }
-    const auto t_out = clk::now();
-    ctx->t_host[0] = ms(t0, t_enq);
-    ctx->t_host[1] = ms(t_enq, t_wait);
-    ctx->t_host[2] = ms(t_wait, t_copy);
-    ctx->t_host[3] = ms(t_copy, t_fin);
-    ctx->t_host[4] = ms(t_fin, t_out);
-    *out_kps = kps;
-    *out_n = n;
-    if (out_desc_f32) *out_desc_f32 = df;
-
-    ctx->counts.extrema = (int64_t)ctx->lane_n[0][0] + ctx->lane_n[0][1];
-    ctx->counts.refined = (int64_t)ctx->lane_n[1][0] + ctx->lane_n[1][1];
-    ctx->counts.oriented = n_ori;
-    ctx->counts.final_n = (int64_t)n;
-    ctx->counts.octaves = g.octaves;
-    ctx->counts.levels_per_octave = g.n_gauss;
-    ctx->counts.octave0_w = g.W[0];
-    ctx->counts.octave0_h = g.H[0];
-    ctx->last_p = *p;
-    ctx->have_run = true;
+    s.counts.extrema = (int64_t)s.lane_n[0][0] + s.lane_n[0][1];
+    s.counts.refined = (int64_t)s.lane_n[1][0] + s.lane_n[1][1];
+    s.counts.oriented = n_ori;
+    s.counts.final_n = (int64_t)s.n_final;
+    s.counts.octaves = g.octaves;
+    s.counts.levels_per_octave = g.n_gauss;
+    s.counts.octave0_w = g.W[0];
+    s.counts.octave0_h = g.H[0];
+    s.state = kFinalized;
+    ctx->last = (int)(&s - ctx->slots);
     return SIFT_OK;
+}
+
+Slot* slot_of(sift_ctx* ctx, int ticket) {
+    for (Slot& s : ctx->slots)
+        if (s.state != kFree && s.ticket == ticket) return &s;
+    return nullptr;
+}
+
+int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind, int w, int h,
+                int c, const sift_params* p, int want_df, int* ticket) {
+    if (!ctx || !images || !ticket || n_images < 1 || n_images > SIFT_MAX_BATCH) return SIFT_ERR_ARG;
+    if (kind < SIFT_INPUT_F64_HOST || kind > SIFT_INPUT_U8_DEVICE) return SIFT_ERR_ARG;
+    for (int b = 0; b < n_images; ++b)
+        if (!images[b]) return SIFT_ERR_ARG;
+    if (w <= 0 || h <= 0) return SIFT_ERR_ARG;
+    if (c != 1 && c != 3) return SIFT_ERR_CHANNELS;
+    sift_params def;
+    if (!p) {
+        sift_params_default(&def);
+        p = &def;
+    }
+    Slot* sp = nullptr;
+    for (int k = 0; k < kSlots; ++k) {  // a free slot, preferring not the introspected one
+        Slot& s = ctx->slots[(ctx->last + 1 + k + kSlots) % kSlots];
+        if (s.state == kFree) {
+            sp = &s;
+            break;
+        }
+    }
+    if (!sp) return SIFT_ERR_STATE;  // SIFT_MAX_INFLIGHT jobs already in flight
+    Slot& s = *sp;
+    int st = host_plan(p, w, h, c, &s.g, &s.taps_init, s.taps, &s.dp);
+    if (st != SIFT_OK) return st;
+    SIFT_HIP_TRY(hipSetDevice(ctx->device));
+    if (ctx->last == (int)(&s - ctx->slots)) ctx->last = -1;  // its buffers get reused
+    s.n_img = n_images;
+    s.w = w;
+    s.h = h;
+    s.c = c;
+    s.p = *p;
+    s.want_df = want_df != 0;
+    s.ticket = ctx->next_ticket++;
+    if (ctx->next_ticket <= 0) ctx->next_ticket = 1;
+    s.state = kSubmitted;
+    st = enqueue_job(ctx, s, images, kind);
+    if (st != SIFT_OK) {
+        abandon(ctx, s);
+        return st;
+    }
+    *ticket = s.ticket;
+    return SIFT_OK;
+}
+
+int wait_impl(sift_ctx* ctx, Slot& s) {
+    if (s.state == kFinalized) return SIFT_OK;
+    (void)hipSetDevice(ctx->device);
+    const int st = finalize_job(ctx, s);
+    if (st != SIFT_OK) abandon(ctx, s);
+    return st;
+}
+
+// kept records of a finalised job, image-major, into caller storage
+void gather(Slot& s, sift_kp* out, float* df) {
+    const auto t0 = clk::now();
+    // record i's host row: exported -> lane-local index already offset by
+    // host_base at export time (keep holds host positions); bulk -> concatenated
+    if (out)
+        for (size_t i = 0; i < s.n_final; ++i) out[i] = s.rec_src[s.keep[i]];
+    if (df && s.want_df)
+        for (size_t i = 0; i < s.n_final; ++i)
+            std::memcpy(df + i * 128, s.h_df32.p + (size_t)s.keep[i] * 128, 128 * sizeof(float));
+    s.t_host[4] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
 }
 
 }  // namespace
@@ -736,20 +917,26 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) ctx->batch_px_log2 = std::atoi(e);
     if (const char* e = std::getenv("SIFT_KP_LANES")) ctx->lanes = std::atoi(e) == 1 ? 1 : kLanes;
     if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 18;
-    if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stream4, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-        hipMalloc(&ctx->d_ctr, kCtrWords * sizeof(unsigned)) != hipSuccess ||
-        hipHostMalloc(&ctx->h_ctr, 4 * kLanes * sizeof(unsigned)) != hipSuccess ||
-        hipHostMalloc(&ctx->h_stage, sizeof(Stage)) != hipSuccess ||
-        hipMalloc(&ctx->d_stage, sizeof(Stage)) != hipSuccess ||
-        prepare_kernel_attributes() != hipSuccess) {
+    bool ok = hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) ==
+                  hipSuccess &&
+              hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) ==
+                  hipSuccess &&
+              hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_lo) ==
+                  hipSuccess &&
+              hipStreamCreateWithPriority(&ctx->stream4, hipStreamNonBlocking, prio_lo) ==
+                  hipSuccess &&
+              prepare_kernel_attributes() == hipSuccess;
+    for (Slot& s : ctx->slots) {
+        ok = ok && hipMalloc(&s.d_ctr, kCtrWords * sizeof(unsigned)) == hipSuccess &&
+             hipHostMalloc(&s.h_ctr, 4 * kLanes * sizeof(unsigned)) == hipSuccess &&
+             hipHostMalloc(&s.h_stage, sizeof(Stage)) == hipSuccess &&
+             hipMalloc(&s.d_stage, sizeof(Stage)) == hipSuccess &&
+             hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming) == hipSuccess;
+    }
+    if (!ok) {
         sift_hip_destroy(ctx);
         return SIFT_ERR_HIP;
     }
-    ctx->d_pt = &ctx->d_stage->pt;
-    ctx->d_taps = ctx->d_stage->taps;
     *out = ctx;
     return SIFT_OK;
 }
@@ -757,66 +944,115 @@ int sift_hip_create(int device, sift_ctx** out) {
 int sift_hip_destroy(sift_ctx* ctx) {
     if (!ctx) return SIFT_ERR_ARG;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
-    if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
-    if (ctx->stream4) (void)hipStreamSynchronize(ctx->stream4);
-    void* bufs[] = {ctx->d_in, ctx->d_pyr, ctx->d_tmp, ctx->d_cand, ctx->d_raw,
-                    ctx->d_ori, ctx->d_off0, ctx->d_df32, ctx->d_ctr, ctx->d_stage,
-                    ctx->d_mbuf};
-    for (void* b : bufs)
-        if (b) (void)hipFree(b);
-    if (ctx->h_ctr) (void)hipHostFree(ctx->h_ctr);
-    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-    ctx->h_ori.release();
-    ctx->exp_rec.release();
-    ctx->exp_off0.release();
-    ctx->exp_cnt.release();
-    for (hipEvent_t e : ctx->chain_ev) (void)hipEventDestroy(e);
-    ctx->h_off0.release();
-    ctx->h_df32.release();
+    for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4})
+        if (st) (void)hipStreamSynchronize(st);
+    for (Slot& s : ctx->slots) {
+        s.in.release();
+        s.in8.release();
+        s.pyr.release();
+        s.tmp.release();
+        s.cand.release();
+        s.raw.release();
+        s.ori.release();
+        s.side.release();
+        s.df32.release();
+        if (s.d_ctr) (void)hipFree(s.d_ctr);
+        if (s.d_stage) (void)hipFree(s.d_stage);
+        if (s.h_ctr) (void)hipHostFree(s.h_ctr);
+        if (s.h_stage) (void)hipHostFree(s.h_stage);
+        s.h_up.release();
+        s.exp_rec.release();
+        s.exp_side.release();
+        s.exp_cnt.release();
+        s.h_ori.release();
+        s.h_side.release();
+        s.h_df32.release();
+        for (hipEvent_t e : s.chain_ev) (void)hipEventDestroy(e);
+        for (hipEvent_t e : s.sync_ev) (void)hipEventDestroy(e);
+        for (hipEvent_t e : s.ev_pool) (void)hipEventDestroy(e);
+        if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+    }
+    if (ctx->d_mbuf) (void)hipFree(ctx->d_mbuf);
     ctx->h_mj.release();
     ctx->h_md.release();
-    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
-    if (ctx->stream4) (void)hipStreamDestroy(ctx->stream4);
+    for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4})
+        if (st) (void)hipStreamDestroy(st);
     delete ctx;
     return SIFT_OK;
+}
+
+int sift_hip_submit(sift_ctx* ctx, const void* const* images, int n_images, int input_kind,
+                    int w, int h, int c, const sift_params* p, int want_desc_f32, int* ticket) {
+    return submit_impl(ctx, images, n_images, input_kind, w, h, c, p, want_desc_f32, ticket);
+}
+
+int sift_hip_wait(sift_ctx* ctx, int ticket, size_t* counts, size_t* total) {
+    if (!ctx) return SIFT_ERR_ARG;
+    Slot* s = slot_of(ctx, ticket);
+    if (!s) return SIFT_ERR_STATE;
+    const int st = wait_impl(ctx, *s);
+    if (st != SIFT_OK) return st;
+    if (counts)
+        for (int b = 0; b < s->n_img; ++b) counts[b] = s->img_count[b];
+    if (total) *total = s->n_final;
+    return SIFT_OK;
+}
+
+int sift_hip_fetch(sift_ctx* ctx, int ticket, sift_kp* out, float* desc_f32) {
+    if (!ctx) return SIFT_ERR_ARG;
+    Slot* s = slot_of(ctx, ticket);
+    if (!s) return SIFT_ERR_STATE;
+    int st = wait_impl(ctx, *s);
+    if (st != SIFT_OK) return st;
+    gather(*s, out, desc_f32);
+    s->state = kFree;
+    s->ticket = -1;
+    return SIFT_OK;
+}
+
+int sift_hip_detect_batch(sift_ctx* ctx, const void* const* images, int n_images,
+                          int input_kind, int w, int h, int c, const sift_params* p,
+                          sift_kp** out_kps, size_t* counts, float** out_desc_f32) {
+    if (!out_kps || !counts) return SIFT_ERR_ARG;
+    *out_kps = nullptr;
+    if (out_desc_f32) *out_desc_f32 = nullptr;
+    int ticket = 0;
+    int st = submit_impl(ctx, images, n_images, input_kind, w, h, c, p, out_desc_f32 != nullptr,
+                         &ticket);
+    if (st != SIFT_OK) return st;
+    size_t n = 0;
+    if ((st = sift_hip_wait(ctx, ticket, counts, &n)) != SIFT_OK) return st;
+    sift_kp* kps = (sift_kp*)std::malloc(std::max<size_t>(n, 1) * sizeof(sift_kp));
+    float* df = out_desc_f32 ? (float*)std::malloc(std::max<size_t>(n, 1) * 128 * sizeof(float))
+                             : nullptr;
+    if (!kps || (out_desc_f32 && !df)) {
+        std::free(kps);
+        std::free(df);
+        (void)sift_hip_fetch(ctx, ticket, nullptr, nullptr);
+        return SIFT_ERR_NOMEM;
+    }
+    st = sift_hip_fetch(ctx, ticket, kps, df);
+    *out_kps = kps;
+    if (out_desc_f32) *out_desc_f32 = df;
+    return st;
 }
 
 int sift_hip_detect(sift_ctx* ctx, const double* hwc, int w, int h, int c,
                     const sift_params* p, sift_kp** out_kps, size_t* out_n,
                     float** out_desc_f32) {
     if (!ctx || !hwc || !out_kps || !out_n) return SIFT_ERR_ARG;
-    if (w <= 0 || h <= 0) return SIFT_ERR_ARG;
-    if (c != 1 && c != 3) return SIFT_ERR_CHANNELS;
-    sift_params def;
-    if (!p) {
-        sift_params_default(&def);
-        p = &def;
-    }
-    SIFT_HIP_TRY(hipSetDevice(ctx->device));
-    const size_t ne = (size_t)w * h * c;
-    int st = ensure(&ctx->d_in, &ctx->in_cap, ne);
-    if (st != SIFT_OK) return st;
-    SIFT_HIP_TRY(hipMemcpyAsync(ctx->d_in, hwc, ne * sizeof(double), hipMemcpyHostToDevice,
-                                ctx->stream));
-    return detect_impl(ctx, ctx->d_in, w, h, c, p, out_kps, out_n, out_desc_f32);
+    const void* img = hwc;
+    return sift_hip_detect_batch(ctx, &img, 1, SIFT_INPUT_F64_HOST, w, h, c, p, out_kps, out_n,
+                                 out_desc_f32);
 }
 
 int sift_hip_detect_device(sift_ctx* ctx, const double* d_hwc, int w, int h, int c,
                            const sift_params* p, sift_kp** out_kps, size_t* out_n,
                            float** out_desc_f32) {
     if (!ctx || !d_hwc || !out_kps || !out_n) return SIFT_ERR_ARG;
-    sift_params def;
-    if (!p) {
-        sift_params_default(&def);
-        p = &def;
-    }
-    return detect_impl(ctx, d_hwc, w, h, c, p, out_kps, out_n, out_desc_f32);
+    const void* img = d_hwc;
+    return sift_hip_detect_batch(ctx, &img, 1, SIFT_INPUT_F64_DEVICE, w, h, c, p, out_kps, out_n,
+                                 out_desc_f32);
 }
 
 namespace {
@@ -825,7 +1061,7 @@ namespace {
 // record lists -> shifted rows + norms, one 2-NN launch, per-query results
 // back to the host, compacted in query order.
 static int match_impl(sift_ctx* ctx, const sift_kp* k1, size_t n1, const sift_kp* k2, size_t n2,
-               bool on_device, double ratio, sift_match_pair** out, size_t* n_out) {
+                      bool on_device, double ratio, sift_match_pair** out, size_t* n_out) {
     if (!ctx || !out || !n_out) return SIFT_ERR_ARG;
     *out = nullptr;
     *n_out = 0;
@@ -921,29 +1157,38 @@ const char* sift_hip_strerror(int status) {
         case SIFT_ERR_NOMEM: return "out of memory";
         case SIFT_ERR_NO_DEVICE: return "no such HIP device";
         case SIFT_ERR_PARAM: return "parameter outside the supported range";
-        case SIFT_ERR_STATE: return "no previous detect on this context";
+        case SIFT_ERR_STATE: return "invalid call order (no such job / no previous detect / too many jobs in flight)";
         default: return "unknown error";
     }
 }
 
+namespace {
+Slot* last_slot(sift_ctx* ctx) {
+    if (!ctx || ctx->last < 0) return nullptr;
+    return &ctx->slots[ctx->last];
+}
+}  // namespace
+
 int sift_hip_last_counts(sift_ctx* ctx, sift_counts* out) {
     if (!ctx || !out) return SIFT_ERR_ARG;
-    if (!ctx->have_run) return SIFT_ERR_STATE;
-    *out = ctx->counts;
+    Slot* s = last_slot(ctx);
+    if (!s) return SIFT_ERR_STATE;
+    *out = s->counts;
     return SIFT_OK;
 }
 
 int sift_hip_copy_level(sift_ctx* ctx, int octave, int level, double* host_out,
                         size_t cap_elems, int* w_out, int* h_out) {
     if (!ctx || !host_out) return SIFT_ERR_ARG;
-    if (!ctx->have_run) return SIFT_ERR_STATE;
-    if (octave < 0 || octave >= ctx->counts.octaves || level < 0 ||
-        level >= ctx->counts.levels_per_octave)
+    Slot* s = last_slot(ctx);
+    if (!s) return SIFT_ERR_STATE;
+    if (octave < 0 || octave >= s->counts.octaves || level < 0 ||
+        level >= s->counts.levels_per_octave)
         return SIFT_ERR_ARG;
-    const int W = ctx->h_pt.w[octave], H = ctx->h_pt.h[octave];
+    const int W = s->h_pt.w[octave], H = s->h_pt.h[octave];
     if (cap_elems < (size_t)W * H) return SIFT_ERR_ARG;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
-    SIFT_HIP_TRY(hipMemcpyAsync(host_out, ctx->h_pt.lvl[octave][level],
+    SIFT_HIP_TRY(hipMemcpyAsync(host_out, s->h_pt.lvl[octave][level],
                                 (size_t)W * H * sizeof(double), hipMemcpyDeviceToHost,
                                 ctx->stream));
     SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -954,16 +1199,17 @@ int sift_hip_copy_level(sift_ctx* ctx, int octave, int level, double* host_out,
 
 int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out, size_t cap, size_t* n_out) {
     if (!ctx || !n_out) return SIFT_ERR_ARG;
-    if (!ctx->have_run) return SIFT_ERR_STATE;
-    const size_t n = (size_t)ctx->counts.extrema;
+    Slot* s = last_slot(ctx);
+    if (!s) return SIFT_ERR_STATE;
+    const size_t n = (size_t)s->counts.extrema;
     *n_out = n;
     if (!host_out) return SIFT_OK;
     if (cap < n) return SIFT_ERR_ARG;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
-    for (int L = 0, off = 0; L < kLanes; off += ctx->lane_n[0][L], ++L)
-        if (ctx->lane_n[0][L])
-            SIFT_HIP_TRY(hipMemcpyAsync(host_out + off, ctx->d_cand + (size_t)L * ctx->cap_cand,
-                                        ctx->lane_n[0][L] * sizeof(sift_extremum),
+    for (int L = 0, off = 0; L < kLanes; off += s->lane_n[0][L], ++L)
+        if (s->lane_n[0][L])
+            SIFT_HIP_TRY(hipMemcpyAsync(host_out + off, s->cand.p + (size_t)L * s->cap_cand,
+                                        s->lane_n[0][L] * sizeof(sift_extremum),
                                         hipMemcpyDeviceToHost, ctx->stream));
     SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return SIFT_OK;
@@ -971,17 +1217,18 @@ int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out, size_t cap, si
 
 int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t* n_out) {
     if (!ctx || !n_out) return SIFT_ERR_ARG;
-    if (!ctx->have_run) return SIFT_ERR_STATE;
-    const size_t n = (size_t)ctx->counts.oriented;
+    Slot* s = last_slot(ctx);
+    if (!s) return SIFT_ERR_STATE;
+    const size_t n = (size_t)s->counts.oriented;
     *n_out = n;
     if (!d_dst) return SIFT_OK;
     if (cap < n) return SIFT_ERR_ARG;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
-    for (int L = 0, off = 0; L < kLanes; off += ctx->lane_n[2][L], ++L)
-        if (ctx->lane_n[2][L])
+    for (int L = 0, off = 0; L < kLanes; off += s->lane_n[2][L], ++L)
+        if (s->lane_n[2][L])
             SIFT_HIP_TRY(hipMemcpyAsync(static_cast<sift_kp*>(d_dst) + off,
-                                        ctx->d_ori + (size_t)L * ctx->cap_ori,
-                                        ctx->lane_n[2][L] * sizeof(sift_kp),
+                                        s->ori.p + (size_t)L * s->cap_ori,
+                                        s->lane_n[2][L] * sizeof(sift_kp),
                                         hipMemcpyDeviceToDevice, ctx->stream));
     SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return SIFT_OK;
@@ -989,8 +1236,9 @@ int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t*
 
 int sift_hip_last_timing(sift_ctx* ctx, double* ms, int n) {
     if (!ctx || !ms || n < 0) return SIFT_ERR_ARG;
-    if (!ctx->have_run) return SIFT_ERR_STATE;
-    for (int i = 0; i < n && i < 5; ++i) ms[i] = ctx->t_host[i];
+    Slot* s = last_slot(ctx);
+    if (!s) return SIFT_ERR_STATE;
+    for (int i = 0; i < n && i < 5; ++i) ms[i] = s->t_host[i];
     return SIFT_OK;
 }
 

@@ -4,8 +4,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 namespace sift_amd {
@@ -109,14 +111,13 @@ int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* 
     return SIFT_OK;
 }
 
-void host_sizes(const sift_params* p, sift_kp* recs, const double* off0, unsigned b,
-                unsigned e) {
-    for (unsigned i = b; i < e; ++i) {
+void host_sizes(const sift_params* p, sift_kp* recs, const RecSide* side, size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
         sift_kp& r = recs[i];
         // std::pow(2, octave) is exactly 2^octave; ldexp gives the same value
         const double scale = std::ldexp(1.0, r.octave);
         double size = p->init_sigma * scale *
-                      std::pow(2, (static_cast<double>(r.layer) + off0[i]) / p->intervals);
+                      std::pow(2, (static_cast<double>(r.layer) + side[i].off0) / p->intervals);
         if (p->double_image_size) size /= 2;
         r.size = size;
     }
@@ -124,9 +125,10 @@ void host_sizes(const sift_params* p, sift_kp* recs, const double* off0, unsigne
 
 namespace {
 
-// Keypoint::operator< (sift.hh:31-41): x asc, y asc, size desc, pori asc,
-// octave desc
+// image, then Keypoint::operator< (sift.hh:31-41): x asc, y asc, size desc,
+// pori asc, octave desc
 bool key_less(const FinalizeKey& a, const FinalizeKey& b) {
+    if (a.img != b.img) return a.img < b.img;
     if (a.x != b.x) return a.x < b.x;
     if (a.y != b.y) return a.y < b.y;
     if (a.size != b.size) return a.size > b.size;
@@ -136,48 +138,55 @@ bool key_less(const FinalizeKey& a, const FinalizeKey& b) {
 
 }  // namespace
 
-void host_sort_run(const sift_kp* recs, unsigned b, unsigned e, FinalizeKey* out,
-                   FinalizeWorkspace* ws) {
-    // Sort a compact key array (40 B per record) in Keypoint::operator<
-    // order. x >= 0 for every keypoint, and bucket(x) = x / x_max * B is
-    // monotone non-decreasing under round-to-nearest, so a stable bucket
-    // pass followed by a comparator sort inside each (tiny) bucket yields
-    // exactly the order std::sort with the full comparator would, in O(n + B).
+void host_sort_run(const sift_kp* recs, const RecSide* side, unsigned b, unsigned e,
+                   FinalizeKey* out, FinalizeWorkspace* ws) {
+    // Sort a compact key array (48 B per record) by (image, Keypoint::
+    // operator<). x >= 0 for every keypoint, and bucket(x) = x / x_max * B
+    // is monotone non-decreasing under round-to-nearest, so a stable pass
+    // over the buckets (image-major, then x) followed by a comparator sort
+    // inside each (tiny) bucket yields exactly the order std::sort with the
+    // full comparator would, in O(n + buckets).
     using Key = FinalizeKey;
     const unsigned n = e - b;
     std::vector<Key>& keys = ws->keys;
     keys.resize(n);
     double x_max = 0.0;
+    int img_max = 0;
     for (unsigned i = 0; i < n; ++i) {
         const sift_kp& r = recs[b + i];
-        keys[i] = {r.x, r.y, r.size, r.pori, r.octave, b + i};
+        const int im = side[b + i].img;
+        keys[i] = {r.x, r.y, r.size, r.pori, r.octave, im, b + i};
         x_max = std::max(x_max, r.x);
+        img_max = std::max(img_max, im);
     }
-    const size_t B = std::max<size_t>(1, std::min<size_t>(n, (size_t)1 << 20));
+    const size_t n_img = (size_t)img_max + 1;
+    const size_t B = std::max<size_t>(1, std::min<size_t>(n, (size_t)1 << 20) / n_img);
     std::vector<unsigned>& start = ws->start;
-    start.assign(B + 1, 0);
-    auto bucket = [&](double x) -> size_t {
-        if (!(x_max > 0.0)) return 0;
-        const double f = x / x_max * (double)B;
-        return f >= (double)(B - 1) ? B - 1 : (f <= 0.0 ? 0 : (size_t)f);
+    start.assign(n_img * B + 1, 0);
+    auto bucket = [&](const Key& k) -> size_t {
+        size_t xb = 0;
+        if (x_max > 0.0) {
+            const double f = k.x / x_max * (double)B;
+            xb = f >= (double)(B - 1) ? B - 1 : (f <= 0.0 ? 0 : (size_t)f);
+        }
+        return (size_t)k.img * B + xb;
     };
-    for (unsigned i = 0; i < n; ++i) ++start[bucket(keys[i].x) + 1];
-    for (size_t q = 0; q < B; ++q) start[q + 1] += start[q];
+    for (unsigned i = 0; i < n; ++i) ++start[bucket(keys[i]) + 1];
+    for (size_t q = 0; q < n_img * B; ++q) start[q + 1] += start[q];
     {
         std::vector<unsigned>& fill = ws->fill;
         fill.assign(start.begin(), start.end() - 1);
-        for (unsigned i = 0; i < n; ++i) out[fill[bucket(keys[i].x)]++] = keys[i];
+        for (unsigned i = 0; i < n; ++i) out[fill[bucket(keys[i])]++] = keys[i];
     }
-    for (size_t q = 0; q < B; ++q) {
+    for (size_t q = 0; q < n_img * B; ++q) {
         Key* lo = out + start[q];
         Key* hi = out + start[q + 1];
         if (hi - lo > 1) std::sort(lo, hi, key_less);
     }
 }
 
-size_t host_merge_unique(const sift_kp* recs, FinalizeKey* keys,
-                         const std::vector<unsigned>& run_start, unsigned* keep,
-                         FinalizeWorkspace* ws) {
+size_t host_merge_unique(FinalizeKey* keys, const std::vector<unsigned>& run_start,
+                         unsigned* keep, size_t* per_img, FinalizeWorkspace* ws) {
     // pairwise merges of the sorted runs [run_start[i], run_start[i+1])
     std::vector<unsigned> bounds(run_start);
     const unsigned n = bounds.empty() ? 0 : bounds.back();
@@ -202,26 +211,62 @@ size_t host_merge_unique(const sift_kp* recs, FinalizeKey* keys,
         std::swap(src, dst);
     }
     size_t m = 0;
+    const FinalizeKey* last = nullptr;
     for (unsigned i = 0; i < n; ++i) {
         const FinalizeKey& k = src[i];
-        if (m > 0) {
-            // std::unique compares with the last kept element (Keypoint::
-            // operator==, sift.hh:25-27: x, y, size, pori)
-            const sift_kp& last = recs[keep[m - 1]];
-            if (last.x == k.x && last.y == k.y && last.size == k.size && last.pori == k.pori)
-                continue;
-        }
+        // std::unique compares with the last kept element (Keypoint::
+        // operator==, sift.hh:25-27: x, y, size, pori), within one image
+        if (last && last->img == k.img && last->x == k.x && last->y == k.y &&
+            last->size == k.size && last->pori == k.pori)
+            continue;
         keep[m++] = k.idx;
+        if (per_img) ++per_img[k.img];
+        last = &k;
     }
     return m;
 }
 
-size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
-                     unsigned* keep, FinalizeWorkspace* ws) {
-    host_sizes(p, recs, off0, 0, n);
+size_t host_finalize(const sift_params* p, sift_kp* recs, const RecSide* side, unsigned n,
+                     unsigned* keep, size_t* per_img, FinalizeWorkspace* ws) {
+    host_sizes(p, recs, side, 0, n);
     ws->all.resize(n);
-    host_sort_run(recs, 0, n, ws->all.data(), ws);
-    return host_merge_unique(recs, ws->all.data(), {0u, n}, keep, ws);
+    host_sort_run(recs, side, 0, n, ws->all.data(), ws);
+    return host_merge_unique(ws->all.data(), {0u, n}, keep, per_img, ws);
+}
+
+namespace {
+
+bool pack_range(const double* src, size_t n, uint8_t* dst) {
+    bool ok = true;
+    for (size_t i = 0; i < n; ++i) {
+        const double v = src[i];
+        const uint8_t u = (v >= 0.0 && v <= 255.0) ? (uint8_t)v : 0;
+        const double back = (double)u;
+        ok &= std::memcmp(&back, &v, sizeof v) == 0;  // bit-identical round trip
+        dst[i] = u;
+    }
+    return ok;
+}
+
+}  // namespace
+
+bool host_pack_u8(const double* src, size_t n, uint8_t* dst) {
+    const size_t kChunk = (size_t)1 << 19;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned nt = (unsigned)std::min<size_t>({(size_t)8, (size_t)hw, (n + kChunk - 1) / kChunk});
+    if (nt <= 1) return pack_range(src, n, dst);
+    std::vector<std::thread> th;
+    std::vector<char> ok(nt, 1);
+    const size_t per = (n + nt - 1) / nt;
+    for (unsigned t = 1; t < nt; ++t) {
+        const size_t b = std::min(n, t * per), e = std::min(n, b + per);
+        th.emplace_back([=, &ok] { ok[t] = pack_range(src + b, e - b, dst + b); });
+    }
+    ok[0] = pack_range(src, std::min(n, per), dst);
+    for (auto& t : th) t.join();
+    for (char c : ok)
+        if (!c) return false;
+    return true;
 }
 
 }  // namespace sift_amd

@@ -31,31 +31,37 @@ int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* 
 
 // Final keypoint size with glibc pow (sift.cpp:427-429, halved at
 // sift.cpp:525) written into recs[i].size for i in [b, e).
-void host_sizes(const sift_params* p, sift_kp* recs, const double* off0, unsigned b,
-                unsigned e);
+void host_sizes(const sift_params* p, sift_kp* recs, const RecSide* side, size_t b, size_t e);
 
 // clean_keypoints (sift.cpp:20-24) in pieces, so a detect can sort the
 // records of each keypoint batch while the device still works on the next:
-// host_sort_run sorts the keys of records [b, e) (Keypoint::operator<,
-// sift.hh:31-41) into out[0, e-b); host_merge_unique merges consecutive
-// sorted runs of `keys` (boundaries run_start, last = total) and applies
-// std::unique (sift.hh:25-27), writing the kept record indices to keep[].
+// host_sort_run sorts the keys of records [b, e) into out[0, e-b) by image,
+// then Keypoint::operator< (sift.hh:31-41); host_merge_unique merges
+// consecutive sorted runs of `keys` (boundaries run_start, last = total) and
+// applies std::unique (sift.hh:25-27) within each image, writing the kept
+// record indices to keep[] (image-major) and counting them per image.
 struct FinalizeKey {
     double x, y, size, pori;
     int octave;
+    int img;
     unsigned idx;
 };
 struct FinalizeWorkspace {  // reused across calls
     std::vector<FinalizeKey> keys, sorted, all;
     std::vector<unsigned> start, fill;
 };
-void host_sort_run(const sift_kp* recs, unsigned b, unsigned e, FinalizeKey* out,
-                   FinalizeWorkspace* ws);
-size_t host_merge_unique(const sift_kp* recs, FinalizeKey* keys,
-                         const std::vector<unsigned>& run_start, unsigned* keep,
-                         FinalizeWorkspace* ws);
+void host_sort_run(const sift_kp* recs, const RecSide* side, unsigned b, unsigned e,
+                   FinalizeKey* out, FinalizeWorkspace* ws);
+size_t host_merge_unique(FinalizeKey* keys, const std::vector<unsigned>& run_start,
+                         unsigned* keep, size_t* per_img, FinalizeWorkspace* ws);
 // all of it over records [0, n): sizes, one run, merge/unique
-size_t host_finalize(const sift_params* p, sift_kp* recs, const double* off0, unsigned n,
-                     unsigned* keep, FinalizeWorkspace* ws);
+size_t host_finalize(const sift_params* p, sift_kp* recs, const RecSide* side, unsigned n,
+                     unsigned* keep, size_t* per_img, FinalizeWorkspace* ws);
+
+// Parallel host pass of the u8 upload path: dst[i] = (uint8_t)src[i] for
+// every i when each src[i] is exactly an integer 0..255 (+0.0 only), which
+// is what an stb-decoded Image holds (image_io.cpp:20-35); returns false
+// (dst unspecified) otherwise.
+bool host_pack_u8(const double* src, size_t n, uint8_t* dst);
 
 }  // namespace sift_amd

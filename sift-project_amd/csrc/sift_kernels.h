@@ -17,24 +17,34 @@ struct BlurShape {
 BlurShape blur_shape_for(int W, int H, int R);
 hipError_t prepare_kernel_attributes();
 
-hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double* out,
-                          int W0, int H0, hipStream_t s);
-// e0/e1: optional HIP events timestamped by the dispatch itself (profiling)
-hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurTaps& taps,
-                       double* dec, int Wd, int Hd, double* tmp, hipStream_t s, hipEvent_t e0,
-                       hipEvent_t e1);
-// Initial blur fused with gray/bilinear-x2 staging from the input image.
-// Returns false (nothing launched) when the fused path does not apply.
-bool launch_blur_initial_fused(const double* in, int w, int h, int c, int dbl, double* dst,
-                               int W0, int H0, const BlurTaps& taps, hipStream_t s,
-                               hipEvent_t e0, hipEvent_t e1, hipError_t* err);
+// Batched launches: n_img images of one job, image b's planes `bs` doubles
+// after image 0's (src, dst and dec alike), blockIdx.z = image.
+hipError_t launch_u8_to_f64(const uint8_t* in, double* out, size_t n, hipStream_t s);
+hipError_t launch_prepare(const double* in, size_t in_bs, int w, int h, int c, int dbl,
+                          double* out, size_t out_bs, int W0, int H0, int n_img, hipStream_t s);
+// e0/e1: optional HIP events timestamped by the dispatch itself (profiling);
+// tmp: n_img * W * H doubles for kernels wider than kMaxTemplR
+hipError_t launch_blur(const double* src, size_t src_bs, double* dst, size_t bs, int n_img, int W,
+                       int H, const BlurTaps& taps, double* dec, int Wd, int Hd, double* tmp,
+                       hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+// Initial blur fused with gray/bilinear-x2 staging from the input images
+// (image b at in + b * in_bs). Returns false (nothing launched) when the
+// fused path does not apply.
+bool launch_blur_initial_fused(const double* in, size_t in_bs, int w, int h, int c, int dbl,
+                               double* dst, size_t bs, int n_img, int W0, int H0,
+                               const BlurTaps& taps, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                               hipError_t* err);
+// every octave in [o_first, o_last] of every image (one workgroup per image)
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
-                              const BlurTaps* d_taps, hipStream_t s, hipEvent_t e0,
+                              const BlurTaps* d_taps, int n_img, hipStream_t s, hipEvent_t e0,
                               hipEvent_t e1);
-hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
-                                int thr, sift_extremum* out, unsigned* counter, unsigned cap,
-                                hipStream_t s);
-hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
+// snap (optional): the last workgroup writes the lane counter snapshot
+// (candidate end, raw / record begins) for the keypoint chain; snap[3] must
+// be zero before the launch.
+hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
+                                int n_gauss, int thr, sift_extremum* out, unsigned* counter,
+                                unsigned cap, unsigned* snap, hipStream_t s);
+hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_img, int n_gauss,
                               int window_size, int thr, sift_extremum* out, unsigned* counter,
                               unsigned cap, hipStream_t s);
 // Keypoint stages process the index range [*begin, *end) of their input
@@ -51,10 +61,10 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 // descriptor launch's record range.
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
-                         sift_kp* recs, double* rec_off0, unsigned* n_rec, unsigned cap_rec,
+                         sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
                          unsigned* work, unsigned wgs, hipStream_t s);
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
-                             const double* rec_off0, const unsigned* rec_begin,
+                             const RecSide* rec_side, const unsigned* rec_begin,
                              const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
                              unsigned* work, const ExportSink& ex, unsigned wgs,
                              hipStream_t s);

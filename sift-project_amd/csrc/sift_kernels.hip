@@ -47,19 +47,26 @@ __device__ __forceinline__ double pow2i(int e) { return ldexp(1.0, e); }
 typedef __attribute__((address_space(1))) const double gdouble;
 __device__ __forceinline__ gdouble* gbl(const double* p) { return (gdouble*)p; }
 
+// Plane of level l of octave o of image b of the job (one pyramid arena per
+// image, identical layouts img_stride doubles apart).
+__device__ __forceinline__ const double* plane(const PyrTable* pt, int b, int o, int l) {
+    return pt->lvl[o][l] + (size_t)b * pt->img_stride;
+}
+
 // XCD-aware block remap (bijective): workgroups are dealt round-robin over
 // the 8 XCDs, so consecutive block ids land on different L2s. Renumber so
 // every XCD owns one contiguous range of logical tiles; neighbouring strips
 // (which re-read each other's halo columns / priming rows) then share an L2.
 // Placement is a speed hint only; results do not depend on it.
-__device__ __forceinline__ void xcd_remap(int& bx, int& by) {
-    const int nx = gridDim.x;
-    const int n = gridDim.x * gridDim.y;
-    const int orig = blockIdx.y * nx + blockIdx.x;
+__device__ __forceinline__ void xcd_remap(int& bx, int& by, int& bz) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int n = nx * ny * gridDim.z;
+    const int orig = (blockIdx.z * ny + blockIdx.y) * nx + blockIdx.x;
     const int q = n / 8, r = n % 8, xcd = orig % 8;
     const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
     bx = id % nx;
-    by = id / nx;
+    by = (id / nx) % ny;
+    bz = id / (nx * ny);
 }
 
 // Source of the rows staged by k_blur: a Gaussian plane, or — for the
@@ -94,12 +101,15 @@ __device__ __forceinline__ double fetch_src(const BlurSource& s, int W, int yy, 
 // convert_to_grayscale (image.cpp:8-24) then resize_inter_bilinear x2
 // (image.cpp:62-88), fused; one thread per output pixel.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_prepare(const double* __restrict__ in, int w,
-                                                 int h, int c, int dbl,
-                                                 double* __restrict__ out, int W0, int H0) {
+__global__ __launch_bounds__(256) void k_prepare(const double* __restrict__ in, size_t in_bs,
+                                                 int w, int h, int c, int dbl,
+                                                 double* __restrict__ out, size_t out_bs,
+                                                 int W0, int H0) {
     const int ox = blockIdx.x * blockDim.x + threadIdx.x;
     const int oy = blockIdx.y;
     if (ox >= W0 || oy >= H0) return;
+    in += blockIdx.z * in_bs;
+    out += blockIdx.z * out_bs;
     auto gray = [&](int x, int y) -> double {
         const double* p = in + ((size_t)y * w + x) * c;
         if (c == 1) return p[0];
@@ -157,8 +167,8 @@ __device__ __forceinline__ double div_sum_w(double a, double s, double inv) {
 // L2-served) and one write per output pixel.
 // ---------------------------------------------------------------------------
 template <int R, int C, bool DECIM, int MODE>
-__global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict__ dst, int W,
-                                              int H, int rows, BlurTaps taps,
+__global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict__ dst,
+                                              size_t bs, int W, int H, int rows, BlurTaps taps,
                                               double* __restrict__ dec, int Wd, int Hd) {
     constexpr int PF = 2;                          // rows in flight ahead of the staged one
     constexpr int NW = 2 * R + 2;                  // register window depth
@@ -168,8 +178,12 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
     __shared__ __attribute__((aligned(16))) double trash[4][SPAN];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int bx, by;
-    xcd_remap(bx, by);
+    int bx, by, bz;
+    xcd_remap(bx, by, bz);
+    // image bz of the batched launch
+    src.p += bz * src.bstride;
+    dst += bz * bs;
+    if (DECIM) dec += bz * bs;
     const int x0 = bx * SPAN;
     const int y_begin = (by * 4 + wv) * rows;
     if (y_begin >= H) return;  // whole wave leaves; no block barriers below
@@ -396,12 +410,13 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, nt = blockDim.x;
     const int dec_level = n_gauss - 3;
+    const int b = blockIdx.x;                // image of the job
     double* A = lds;                         // current level
     double* T = lds + kLdsOctavePx;          // horizontal-pass temporary
     double* D = lds + 2 * kLdsOctavePx;      // next octave's base
     {
         const int W = pt->w[o_first], H = pt->h[o_first];
-        const double* g0 = pt->lvl[o_first][0];
+        const double* g0 = plane(pt, b, o_first, 0);
         for (int i = tid; i < W * H; i += nt) A[i] = g0[i];
     }
     __syncthreads();
@@ -415,9 +430,9 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
         L.H = pt->h[o];
         L.Wd = has_next ? pt->w[o + 1] : 0;
         L.Hd = has_next ? pt->h[o + 1] : 0;
-        L.gd = has_next ? pt->lvl[o + 1][0] : nullptr;
+        L.gd = has_next ? const_cast<double*>(plane(pt, b, o + 1, 0)) : nullptr;
         for (int l = 1; l < n_gauss; ++l) {
-            L.g = pt->lvl[o][l];
+            L.g = const_cast<double*>(plane(pt, b, o, l));
             L.dec = has_next && l == dec_level;
             const BlurTaps& t = taps[l];
             switch (t.R) {
@@ -444,10 +459,12 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
 // Generic fallbacks for kernels wider than kMaxTemplR (unusual sigmas): a
 // plain horizontal pass into `tmp`, then a vertical pass, one thread per px.
 __global__ __launch_bounds__(256) void k_blur_rows_any(const double* __restrict__ src,
-                                                       double* __restrict__ tmp, int W,
-                                                       int H, BlurTaps tp) {
+                                                       size_t src_bs, double* __restrict__ tmp,
+                                                       int W, int H, BlurTaps tp) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
+    src += blockIdx.z * src_bs;
+    tmp += blockIdx.z * (size_t)W * H;
     const double* row = src + (size_t)y * W;
     double acc = row[x] * tp.k[0];
     for (int u = 1; u <= tp.R; ++u)
@@ -456,12 +473,15 @@ __global__ __launch_bounds__(256) void k_blur_rows_any(const double* __restrict_
 }
 
 __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict__ tmp,
-                                                       double* __restrict__ dst, int W,
-                                                       int H, BlurTaps tp,
+                                                       double* __restrict__ dst, size_t bs,
+                                                       int W, int H, BlurTaps tp,
                                                        double* __restrict__ dec, int Wd,
                                                        int Hd) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
+    tmp += blockIdx.z * (size_t)W * H;
+    dst += blockIdx.z * bs;
+    if (dec) dec += blockIdx.z * bs;
     double acc = tmp[(size_t)y * W + x] * tp.k[0];
     for (int u = 1; u <= tp.R; ++u)
         acc += tp.k[u] * (tmp[(size_t)min(y + u, H - 1) * W + x] +
@@ -486,16 +506,39 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
 // memory round trip), then each thread takes one column x four centre rows
 // and walks the layers with a rolling window of three layers' 3x3 max/min
 // in registers. Candidates are compacted with a 64-bit ballot per
-// (row, layer) and one atomic per wave. (Refining each candidate right here
+// (row, layer) and one atomic per wave. The last workgroup to finish takes
+// the lane's counter snapshot for the keypoint chain (snap != nullptr:
+// candidate end, raw / record begins; snap[3] is the done counter). Image b
+// of the job is blockIdx.y; candidates carry octave | b << kOctBits.
+// (Refining each candidate right here
 // was measured slower: the refine's dependent 27-point gathers serialise in
 // the tile's workgroup, where the separate thread-per-candidate k_refine
 // overlaps them across all candidates.)
+// No memory fence here, deliberately: every candidate atomic of a workgroup
+// has returned (it is performed at the device coherence point) before the
+// workgroup's done increment, so the last workgroup's atomic reads see the
+// final counts; the candidate records and the snapshot reach the next kernel
+// through the kernel boundary. (__threadfence() on gfx950 is an L2 writeback
+// + invalidate of the XCD: one per workgroup tripled the extrema time and
+// evicted the concurrent blurs' lines.)
+__device__ __forceinline__ void snapshot_if_last(unsigned* snap, const unsigned* live) {
+    __syncthreads();
+    if (snap && threadIdx.x == 0) {
+        const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
+        if (atomicAdd(&snap[3], 1u) == nblk - 1) {
+            snap[0] = atomicAdd(const_cast<unsigned*>(&live[0]), 0u);
+            snap[1] = atomicAdd(const_cast<unsigned*>(&live[1]), 0u);
+            snap[2] = atomicAdd(const_cast<unsigned*>(&live[2]), 0u);
+        }
+    }
+}
+
 template <int NL>
 __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restrict__ pt,
                                                        ExtremaGrid eg, int thr,
                                                        sift_extremum* __restrict__ out,
                                                        unsigned* __restrict__ counter,
-                                                       unsigned cap) {
+                                                       unsigned cap, unsigned* snap) {
     constexpr int ND = NL - 1;
     constexpr int TW = 64, TH = 16, SW = TW + 2, SH = TH + 2;
     constexpr int NPIX = SW * SH;             // 1188 staged pixels
@@ -505,10 +548,12 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
     int e = 0;
     while (e + 1 < eg.n && (int)blockIdx.x >= eg.first_tile[e + 1]) ++e;
     const int o = eg.oct[e];
+    const int b = blockIdx.y;
     const int tile = blockIdx.x - eg.first_tile[e];
     const int tx = tile % eg.tiles_x[e], ty = tile / eg.tiles_x[e];
     const int W = pt->w[o], H = pt->h[o];
     const int cx0 = 1 + tx * TW, cy0 = 1 + ty * TH;  // first centre of the tile
+    const int otag = o | (b << kOctBits);
     {
         double g[NIT][NL];
 #pragma unroll
@@ -517,7 +562,7 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
             const int r = i / SW, c = i - r * SW;
             const size_t q = (size_t)clampi(cy0 - 1 + r, 0, H - 1) * W + clampi(cx0 - 1 + c, 0, W - 1);
 #pragma unroll
-            for (int l = 0; l < NL; ++l) g[it][l] = (i < NPIX) ? gbl(pt->lvl[o][l])[q] : 0.0;
+            for (int l = 0; l < NL; ++l) g[it][l] = (i < NPIX) ? gbl(plane(pt, b, o, l))[q] : 0.0;
         }
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
@@ -568,7 +613,7 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
                     if (lane == 0) base = atomicAdd(counter, (unsigned)__popcll(m));
                     base = __shfl(base, 0);
                     const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-                    if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, o};
+                    if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, otag};
                 }
             }
         }
@@ -580,6 +625,7 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
             qmn[k] = nmn[k];
         }
     }
+    snapshot_if_last(snap, counter);
 }
 
 // Generic border b (window_size 4..7): one thread per (x, y), direct cube.
@@ -590,23 +636,24 @@ __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict_
                                                      unsigned cap) {
     const int W = pt->w[o], H = pt->h[o];
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    const int im = blockIdx.z;
     if (x < b || x >= W - b || y < b || y >= H - b) return;
     for (int z = b; z < nd - b; ++z) {
         const size_t c = (size_t)y * W + x;
-        const double v = pt->lvl[o][z + 1][c] - pt->lvl[o][z][c];
+        const double v = plane(pt, im, o, z + 1)[c] - plane(pt, im, o, z)[c];
         if (fabs(v) <= (double)thr) continue;
         bool mx = true, mn = true;
         for (int dz = -b; dz <= b; ++dz)
             for (int dy = -b; dy <= b; ++dy)
                 for (int dx = -b; dx <= b; ++dx) {
                     const size_t q = (size_t)(y + dy) * W + (x + dx);
-                    const double n = pt->lvl[o][z + dz + 1][q] - pt->lvl[o][z + dz][q];
+                    const double n = plane(pt, im, o, z + dz + 1)[q] - plane(pt, im, o, z + dz)[q];
                     if (v < n) mx = false;
                     if (v > n) mn = false;
                 }
         if (mx || mn) {
             const unsigned idx = atomicAdd(counter, 1u);
-            if (idx < cap) out[idx] = sift_extremum{x, y, z, o};
+            if (idx < cap) out[idx] = sift_extremum{x, y, z, o | (im << kOctBits)};
         }
     }
 }
@@ -618,7 +665,7 @@ __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict_
 // the host recomputes with glibc for the final records).
 // ---------------------------------------------------------------------------
 __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, int ex, int ey,
-                           int ez, int o, RawKp* out) {
+                           int ez, int o, int im, RawKp* out) {
     const int b = P.window_size / 2;
     const int W = pt->w[o], H = pt->h[o], depth = P.n_dog;
     double x = ex, y = ey;
@@ -630,8 +677,8 @@ __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, 
         const int xi = (int)x, yi = (int)y;
 #pragma unroll
         for (int dz = -1; dz <= 1; ++dz) {
-            gdouble* ga = gbl(pt->lvl[o][layer + dz + 1]);
-            gdouble* gb = gbl(pt->lvl[o][layer + dz]);
+            gdouble* ga = gbl(plane(pt, im, o, layer + dz + 1));
+            gdouble* gb = gbl(plane(pt, im, o, layer + dz));
 #pragma unroll
             for (int dx = -1; dx <= 1; ++dx)
 #pragma unroll
@@ -686,6 +733,8 @@ __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, 
     out->off0 = off0;
     out->octave = o;
     out->layer = layer;
+    out->img = im;
+    out->pad = 0;
     return true;
 }
 
@@ -704,7 +753,8 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
          i += gridDim.x * blockDim.x) {
         const sift_extremum e = cand[i];
         RawKp r;
-        if (!refine_one(pt, P, e.x, e.y, e.z, e.octave, &r)) continue;
+        const int o = e.octave & ((1 << kOctBits) - 1), im = e.octave >> kOctBits;
+        if (!refine_one(pt, P, e.x, e.y, e.z, o, im, &r)) continue;
         const unsigned idx = atomicAdd(n_out, 1u);
         if (idx < cap_out) out[idx] = r;
     }
@@ -768,12 +818,12 @@ struct KpLds {
 // One descriptor (sift.cpp:610-682) of record `rec`; all 256 threads.
 __device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevParams& P,
                          sift_kp* __restrict__ recs, unsigned rec, double kx, double ky, int o,
-                         int layer, double ksize, double pori, double off0,
+                         int layer, double ksize, double pori, RecSide rside,
                          float* __restrict__ desc_f32, const ExportSink& ex) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     double* hw_rep = &S.hist[(wv * kDescReps + (lane & (kDescReps - 1))) * kDescRepStride];
-    gdouble* img = gbl(pt->lvl[o][layer]);
+    gdouble* img = gbl(plane(pt, rside.img, o, layer));
     const int W = pt->w[o], H = pt->h[o];
     const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
     const int x = (int)(kx * inv);
@@ -971,7 +1021,7 @@ __device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevPar
                 r.layer = layer;
                 r.size = ksize;
                 r.pori = pori;
-                ex.off0[rec] = off0;
+                ex.side[rec] = rside;
             }
         }
     }
@@ -980,7 +1030,7 @@ __device__ void describe(KpLds& S, const PyrTable* __restrict__ pt, const DevPar
 __global__ __launch_bounds__(256) void k_orient(
     const PyrTable* __restrict__ pt, DevParams P, const RawKp* __restrict__ raw,
     const unsigned* __restrict__ raw_begin, const unsigned* __restrict__ n_raw, unsigned cap_raw,
-    sift_kp* __restrict__ recs, double* __restrict__ rec_off0, unsigned* __restrict__ n_rec,
+    sift_kp* __restrict__ recs, RecSide* __restrict__ rec_side, unsigned* __restrict__ n_rec,
     unsigned cap_rec, unsigned* __restrict__ work) {
     __shared__ KpLds S;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1007,7 +1057,7 @@ __global__ __launch_bounds__(256) void k_orient(
         const double scale = P.ori_sigma_factor * size;
         const int radius = (int)round(3.0 * scale);
         const double denom = 2.0 * scale * scale;
-        gdouble* img = gbl(pt->lvl[o][kp.layer]);
+        gdouble* img = gbl(plane(pt, kp.img, o, kp.layer));
         const int W = pt->w[o], H = pt->h[o];
         const int side = 2 * radius + 1;
         for (int i = tid; i < 4 * kOriReps * stride; i += 256) S.hist[i] = 0.0;
@@ -1113,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_orient(
                 r.layer = kp.layer;
                 r.size = rs;
                 r.pori = S.pk[p];
-                rec_off0[rec] = kp.off0;
+                rec_side[rec] = RecSide{kp.off0, kp.img, 0};
             }
         }
         __syncthreads();
@@ -1121,10 +1171,10 @@ __global__ __launch_bounds__(256) void k_orient(
 }
 
 // Descriptors of records [*rec_begin, *n_rec), one workgroup per record
-// from a work counter; the last workgroup to finish publishes the range.
+// from a work counter; workgroup 0 publishes the range.
 __global__ __launch_bounds__(256, 3) void k_descriptor(const PyrTable* __restrict__ pt, DevParams P,
                                                     sift_kp* __restrict__ recs,
-                                                    const double* __restrict__ rec_off0,
+                                                    const RecSide* __restrict__ rec_side,
                                                     const unsigned* __restrict__ rec_begin,
                                                     const unsigned* __restrict__ n_rec,
                                                     unsigned cap_rec, float* __restrict__ desc_f32,
@@ -1133,6 +1183,12 @@ __global__ __launch_bounds__(256, 3) void k_descriptor(const PyrTable* __restric
     const int tid = threadIdx.x;
     const unsigned n = min(*n_rec, cap_rec);
     const unsigned k0 = min(*rec_begin, n);
+    // the launch's record range is fixed before it starts (orientation has
+    // completed); the host reads it after the chain's completion event
+    if (ex.cnt && blockIdx.x == 0 && tid == 0) {
+        ex.cnt[0] = k0;
+        ex.cnt[1] = n;
+    }
     for (;;) {
         if (tid == 0) S.k = k0 + atomicAdd(work, 1u);
         __syncthreads();
@@ -1140,15 +1196,8 @@ __global__ __launch_bounds__(256, 3) void k_descriptor(const PyrTable* __restric
         if (k >= n) break;
         const double* hdr = reinterpret_cast<const double*>(&recs[k]);
         describe(S, pt, P, recs, k, hdr[0], hdr[1], reinterpret_cast<const int*>(hdr)[4],
-                 reinterpret_cast<const int*>(hdr)[5], hdr[3], hdr[4], rec_off0[k], desc_f32, ex);
+                 reinterpret_cast<const int*>(hdr)[5], hdr[3], hdr[4], rec_side[k], desc_f32, ex);
         __syncthreads();
-    }
-    if (ex.cnt && tid == 0) {
-        __threadfence();
-        if (atomicAdd(work + 1, 1u) == gridDim.x - 1) {
-            ex.cnt[0] = k0;
-            ex.cnt[1] = n;
-        }
     }
 }
 
@@ -1168,19 +1217,20 @@ static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, size_t lds, hipS
 }
 
 template <int R, int C, int MODE>
-static hipError_t launch_blur_r(const BlurSource& src, double* dst, int W, int H, int rows,
-                                const BlurTaps& taps, double* dec, int Wd, int Hd,
-                                hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    dim3 grid((W + 64 * C - 1) / (64 * C), ((H + rows - 1) / rows + 3) / 4);
+static hipError_t launch_blur_r(const BlurSource& src, double* dst, size_t bs, int n_img, int W,
+                                int H, int rows, const BlurTaps& taps, double* dec, int Wd,
+                                int Hd, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    dim3 grid((W + 64 * C - 1) / (64 * C), ((H + rows - 1) / rows + 3) / 4, n_img);
     if (MODE == kSrcPlane && dec)
         return launch_timed(k_blur<R, C, true, kSrcPlane>, grid, dim3(256), 0, s, e0, e1, src,
-                            dst, W, H, rows, taps, dec, Wd, Hd);
-    return launch_timed(k_blur<R, C, false, MODE>, grid, dim3(256), 0, s, e0, e1, src, dst, W,
-                        H, rows, taps, dec, Wd, Hd);
+                            dst, bs, W, H, rows, taps, dec, Wd, Hd);
+    return launch_timed(k_blur<R, C, false, MODE>, grid, dim3(256), 0, s, e0, e1, src, dst, bs,
+                        W, H, rows, taps, dec, Wd, Hd);
 }
 
-using BlurFn = hipError_t (*)(const BlurSource&, double*, int, int, int, const BlurTaps&,
-                              double*, int, int, hipStream_t, hipEvent_t, hipEvent_t);
+using BlurFn = hipError_t (*)(const BlurSource&, double*, size_t, int, int, int, int,
+                              const BlurTaps&, double*, int, int, hipStream_t, hipEvent_t,
+                              hipEvent_t);
 
 template <int C, int MODE, int... Rs>
 struct BlurTable {
@@ -1213,37 +1263,40 @@ BlurShape blur_shape_for(int W, int H, int R) {
     return b;
 }
 
-static hipError_t launch_blur_shaped(int MODE, const BlurSource& bs, double* dst, int W, int H,
-                                     const BlurTaps& taps, double* dec, int Wd, int Hd,
-                                     hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static hipError_t launch_blur_shaped(int MODE, const BlurSource& bs, double* dst, size_t dst_bs,
+                                     int n_img, int W, int H, const BlurTaps& taps, double* dec,
+                                     int Wd, int Hd, hipStream_t s, hipEvent_t e0,
+                                     hipEvent_t e1) {
     const BlurShape sh = blur_shape_for(W, H, taps.R);
     const int i = taps.R - 1;
+    BlurFn f;
     if (MODE == kSrcPlane)
-        return (sh.cols == 2 ? BlurPlane2::fns[i] : BlurPlane1::fns[i])(bs, dst, W, H, sh.rows, taps,
-                                                                       dec, Wd, Hd, s, e0, e1);
-    if (MODE == kSrcGray)
-        return (sh.cols == 2 ? BlurGray2::fns[i] : BlurGray1::fns[i])(bs, dst, W, H, sh.rows, taps,
-                                                                     dec, Wd, Hd, s, e0, e1);
-    return (sh.cols == 2 ? BlurUps2::fns[i] : BlurUps1::fns[i])(bs, dst, W, H, sh.rows, taps, dec,
-                                                               Wd, Hd, s, e0, e1);
+        f = sh.cols == 2 ? BlurPlane2::fns[i] : BlurPlane1::fns[i];
+    else if (MODE == kSrcGray)
+        f = sh.cols == 2 ? BlurGray2::fns[i] : BlurGray1::fns[i];
+    else
+        f = sh.cols == 2 ? BlurUps2::fns[i] : BlurUps1::fns[i];
+    return f(bs, dst, dst_bs, n_img, W, H, sh.rows, taps, dec, Wd, Hd, s, e0, e1);
 }
 
-hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurTaps& taps,
-                       double* dec, int Wd, int Hd, double* tmp, hipStream_t s, hipEvent_t e0,
-                       hipEvent_t e1) {
+hipError_t launch_blur(const double* src, size_t src_bs, double* dst, size_t bs, int n_img, int W,
+                       int H, const BlurTaps& taps, double* dec, int Wd, int Hd, double* tmp,
+                       hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const int R = taps.R;
     if (R >= 1 && R <= kMaxTemplR) {
-        const BlurSource bs{src, W, H, 1};
-        return launch_blur_shaped(kSrcPlane, bs, dst, W, H, taps, dec, Wd, Hd, s, e0, e1);
+        const BlurSource src_desc{src, src_bs, W, H, 1};
+        return launch_blur_shaped(kSrcPlane, src_desc, dst, bs, n_img, W, H, taps, dec, Wd, Hd,
+                                  s, e0, e1);
     }
     // wide kernels (or R == 0): generic two-pass path through `tmp`
-    dim3 grid((W + 255) / 256, H);
+    // (n_img * W * H doubles)
+    dim3 grid((W + 255) / 256, H, n_img);
     if (e0) {
         hipError_t e = hipEventRecord(e0, s);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_blur_rows_any, grid, dim3(256), 0, s, src, tmp, W, H, taps);
-    hipLaunchKernelGGL(k_blur_cols_any, grid, dim3(256), 0, s, tmp, dst, W, H, taps, dec,
+    hipLaunchKernelGGL(k_blur_rows_any, grid, dim3(256), 0, s, src, src_bs, tmp, W, H, taps);
+    hipLaunchKernelGGL(k_blur_cols_any, grid, dim3(256), 0, s, tmp, dst, bs, W, H, taps, dec,
                        Wd, Hd);
     if (e1) {
         hipError_t e = hipEventRecord(e1, s);
@@ -1252,14 +1305,15 @@ hipError_t launch_blur(const double* src, double* dst, int W, int H, const BlurT
     return hipGetLastError();
 }
 
-bool launch_blur_initial_fused(const double* in, int w, int h, int c, int dbl, double* dst,
-                               int W0, int H0, const BlurTaps& taps, hipStream_t s,
-                               hipEvent_t e0, hipEvent_t e1, hipError_t* err) {
+bool launch_blur_initial_fused(const double* in, size_t in_bs, int w, int h, int c, int dbl,
+                               double* dst, size_t bs, int n_img, int W0, int H0,
+                               const BlurTaps& taps, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                               hipError_t* err) {
     const int R = taps.R;
     if (R < 1 || R > kMaxTemplR || (c == 1 && !dbl)) return false;
-    const BlurSource bs{in, w, h, c};
-    *err = launch_blur_shaped(dbl ? kSrcUpsample : kSrcGray, bs, dst, W0, H0, taps, nullptr, 0, 0,
-                              s, e0, e1);
+    const BlurSource src_desc{in, in_bs, w, h, c};
+    *err = launch_blur_shaped(dbl ? kSrcUpsample : kSrcGray, src_desc, dst, bs, n_img, W0, H0,
+                              taps, nullptr, 0, 0, s, e0, e1);
     return true;
 }
 
@@ -1270,29 +1324,65 @@ hipError_t prepare_kernel_attributes() {
 }
 
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
-                              const BlurTaps* d_taps, hipStream_t s, hipEvent_t e0,
+                              const BlurTaps* d_taps, int n_img, hipStream_t s, hipEvent_t e0,
                               hipEvent_t e1) {
-    return launch_timed(k_octaves_lds, dim3(1), dim3(1024), kLdsOctaveBytes, s, e0, e1, d_pt,
+    return launch_timed(k_octaves_lds, dim3(n_img), dim3(1024), kLdsOctaveBytes, s, e0, e1, d_pt,
                         o_first, o_last, n_gauss, d_taps);
 }
 
-hipError_t launch_prepare(const double* in, int w, int h, int c, int dbl, double* out,
-                          int W0, int H0, hipStream_t s) {
-    dim3 grid((W0 + 255) / 256, H0);
-    hipLaunchKernelGGL(k_prepare, grid, dim3(256), 0, s, in, w, h, c, dbl, out, W0, H0);
+hipError_t launch_prepare(const double* in, size_t in_bs, int w, int h, int c, int dbl,
+                          double* out, size_t out_bs, int W0, int H0, int n_img, hipStream_t s) {
+    dim3 grid((W0 + 255) / 256, H0, n_img);
+    hipLaunchKernelGGL(k_prepare, grid, dim3(256), 0, s, in, in_bs, w, h, c, dbl, out, out_bs,
+                       W0, H0);
     return hipGetLastError();
 }
 
-hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_gauss,
-                                int thr, sift_extremum* out, unsigned* counter, unsigned cap,
-                                hipStream_t s) {
+// Image bytes -> doubles (exact: every uint8 is a double), 8 per thread.
+__global__ __launch_bounds__(256) void k_u8_to_f64(const uint8_t* __restrict__ in,
+                                                   double* __restrict__ out, size_t n) {
+    const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (i0 + 8 <= n && !((uintptr_t)(in + i0) & 7)) {
+        const uint64_t v = *reinterpret_cast<const uint64_t*>(in + i0);
+        double2* o = reinterpret_cast<double2*>(out + i0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = make_double2((double)((v >> (16 * k)) & 0xFF), (double)((v >> (16 * k + 8)) & 0xFF));
+    } else {
+        for (size_t i = i0; i < n && i < i0 + 8; ++i) out[i] = (double)in[i];
+    }
+}
+
+hipError_t launch_u8_to_f64(const uint8_t* in, double* out, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const size_t threads = (n + 7) / 8;
+    hipLaunchKernelGGL(k_u8_to_f64, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, in,
+                       out, n);
+    return hipGetLastError();
+}
+
+__global__ void k_snapshot(const unsigned* __restrict__ ctr, unsigned* __restrict__ snap, int w0,
+                           int w1) {
+    if ((int)threadIdx.x >= w0 && (int)threadIdx.x < w1) snap[threadIdx.x] = ctr[threadIdx.x];
+}
+
+hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, int w0, int w1) {
+    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(64), 0, s, ctr, snap, w0, w1);
+    return hipGetLastError();
+}
+
+hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
+                                int n_gauss, int thr, sift_extremum* out, unsigned* counter,
+                                unsigned cap, unsigned* snap, hipStream_t s) {
     const int blocks = eg.first_tile[eg.n];
-    if (blocks == 0) return hipSuccess;
+    if (blocks == 0 || n_img == 0)  // nothing to scan: the snapshot is the live counters
+        return snap ? launch_snapshot(counter, snap, s, 0, 3) : hipSuccess;
+    const dim3 grid(blocks, n_img);
     switch (n_gauss) {
-#define SIFT_EXT_CASE(NL)                                                                 \
-    case NL:                                                                              \
-        hipLaunchKernelGGL((k_extrema_tiles<NL>), dim3(blocks), dim3(256), 0, s, d_pt, eg, \
-                           thr, out, counter, cap);                                       \
+#define SIFT_EXT_CASE(NL)                                                                  \
+    case NL:                                                                               \
+        hipLaunchKernelGGL((k_extrema_tiles<NL>), grid, dim3(256), 0, s, d_pt, eg, thr, out, \
+                           counter, cap, snap);                                            \
         return hipGetLastError();
         SIFT_EXT_CASE(4)
         SIFT_EXT_CASE(5)
@@ -1309,23 +1399,13 @@ hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int
     }
 }
 
-hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_gauss,
+hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_img, int n_gauss,
                               int window_size, int thr, sift_extremum* out, unsigned* counter,
                               unsigned cap, hipStream_t s) {
     const int b = window_size / 2;
-    dim3 grid((W + 255) / 256, H);
+    dim3 grid((W + 255) / 256, H, n_img);
     hipLaunchKernelGGL(k_extrema_any, grid, dim3(256), 0, s, d_pt, o, thr, b, n_gauss - 1, out,
                        counter, cap);
-    return hipGetLastError();
-}
-
-__global__ void k_snapshot(const unsigned* __restrict__ ctr, unsigned* __restrict__ snap, int w0,
-                           int w1) {
-    if ((int)threadIdx.x >= w0 && (int)threadIdx.x < w1) snap[threadIdx.x] = ctr[threadIdx.x];
-}
-
-hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, int w0, int w1) {
-    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(64), 0, s, ctr, snap, w0, w1);
     return hipGetLastError();
 }
 
@@ -1342,23 +1422,23 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
-                         sift_kp* recs, double* rec_off0, unsigned* n_rec, unsigned cap_rec,
+                         sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
                          unsigned* work, unsigned wgs, hipStream_t s) {
     unsigned blocks = wgs;  // persistent: workgroups pull keypoints
     if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
     hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), 0, s, d_pt, P, raw, raw_begin, n_raw,
-                       cap_raw, recs, rec_off0, n_rec, cap_rec, work);
+                       cap_raw, recs, rec_side, n_rec, cap_rec, work);
     return hipGetLastError();
 }
 
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
-                             const double* rec_off0, const unsigned* rec_begin,
+                             const RecSide* rec_side, const unsigned* rec_begin,
                              const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
                              unsigned* work, const ExportSink& ex, unsigned wgs,
                              hipStream_t s) {
     unsigned blocks = wgs;  // persistent: workgroups pull records
     if (blocks > cap_rec) blocks = cap_rec > 0 ? cap_rec : 1;
-    hipLaunchKernelGGL(k_descriptor, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_off0,
+    hipLaunchKernelGGL(k_descriptor, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_side,
                        rec_begin, n_rec, cap_rec, desc_f32, work, ex);
     return hipGetLastError();
 }

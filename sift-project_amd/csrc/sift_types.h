@@ -21,6 +21,8 @@ constexpr double kMagThr = 0.2;     // DESC_MAGNITUDE_THR
 constexpr double kIntFactor = 512.0;  // INT_DESCR_FCTR
 
 constexpr int kMaxOctaves = 16;   // floor(log2(min/3)) < 16 for any int image
+constexpr int kOctBits = 4;       // sift_extremum.octave = o | image << kOctBits
+constexpr int kMaxImages = 16;    // images of one job (one batched launch each)
 constexpr int kMaxLevels = 12;    // intervals + 3 with intervals <= 9
 constexpr int kMaxTemplR = 16;    // widest register-window blur kernel (the
                                   // NW-unrolled body stops unrolling past 16)
@@ -42,22 +44,28 @@ struct BlurTaps {
 };
 
 // What k_blur stages rows from: a W x H plane (p, with w = W), or the input
-// image (p = HWC doubles of w x h x c) for the fused initial blur.
+// image (p = HWC doubles of w x h x c) for the fused initial blur. Image b of
+// a batched launch (blockIdx.z) reads p + b * bstride.
 struct BlurSource {
     const double* p;
+    size_t bstride;
     int w, h, c;
 };
 
-// Device-resident table of pyramid level planes.
+// Device-resident table of pyramid level planes of image 0 of a job; image b
+// has the same layout img_stride doubles further (one arena per job).
 struct PyrTable {
     double* lvl[kMaxOctaves][kMaxLevels];
     int w[kMaxOctaves];
     int h[kMaxOctaves];
+    size_t img_stride;
+    int n_img;
+    int n_oct;
 };
 
 // Flattened tile grid of one extrema launch over a set of octaves: entry i
 // (octave oct[i]) owns blocks [first_tile[i], first_tile[i+1]), tiles_x[i]
-// tiles of 64 centre columns per band of 16 centre rows.
+// tiles of 64 centre columns per band of 16 centre rows; blockIdx.y = image.
 struct ExtremaGrid {
     int n;
     int oct[kMaxOctaves];
@@ -85,19 +93,28 @@ struct DevParams {
 };
 
 // Refined keypoint before orientation (sift.cpp:419-430) plus the scale
-// offset, which the host needs to recompute size with glibc pow.
+// offset, which the host needs to recompute size with glibc pow, and the
+// image of the job it belongs to.
 struct RawKp {
     double x, y, size, off0;
     int octave, layer;
+    int img, pad;
 };
 
-// Where k_orient_describe also writes each finished record (mapped, coherent
+// Per-record side data next to the 168-B records: the scale offset (host
+// size with glibc pow) and the image of the job.
+struct RecSide {
+    double off0;
+    int img, pad;
+};
+
+// Where k_descriptor also writes each finished record (mapped, coherent
 // pinned host memory), so the host can finalise a keypoint batch while the
-// device works on the next: rec/off0 index = record index (< cap), cnt =
+// device works on the next: rec/side index = record index (< cap), cnt =
 // this launch's [begin, end) record range.
 struct ExportSink {
     sift_kp* rec;
-    double* off0;
+    RecSide* side;
     unsigned* cnt;
     unsigned cap;
 };

@@ -40,6 +40,11 @@ EXT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("z", "<i4"), ("octave", "<i4"
 # as indices into the two keypoint lists plus the distance
 MATCH_DTYPE = np.dtype([("i1", "<u4"), ("i2", "<u4"), ("distance", "<f8")])
 
+# input kinds of sift_hip_submit (include/sift_hip.h)
+INPUT_F64_HOST, INPUT_F64_DEVICE, INPUT_U8_HOST, INPUT_U8_DEVICE = 0, 1, 2, 3
+MAX_BATCH = 16
+MAX_INFLIGHT = 2
+
 ERRORS = {
     0: "ok",
     -1: "invalid argument",
@@ -49,7 +54,7 @@ ERRORS = {
     -5: "out of memory",
     -6: "no such HIP device",
     -7: "parameter outside the supported range",
-    -8: "no previous detect on this context",
+    -8: "invalid call order (no such job / no previous detect / too many jobs in flight)",
 }
 
 # exported symbols declared in include/sift_hip.h
@@ -61,6 +66,10 @@ EXPORTS = (
     "sift_hip_detect_device",
     "sift_hip_free",
     "sift_hip_strerror",
+    "sift_hip_submit",
+    "sift_hip_wait",
+    "sift_hip_fetch",
+    "sift_hip_detect_batch",
     "sift_hip_match",
     "sift_hip_match_device",
     "sift_hip_last_counts",
@@ -157,6 +166,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sift_hip_free.restype = None
     lib.sift_hip_strerror.argtypes = [i]
     lib.sift_hip_strerror.restype = ctypes.c_char_p
+    lib.sift_hip_submit.argtypes = [vp, ctypes.POINTER(vp), i, i, i, i, i,
+                                    ctypes.POINTER(CParams), i, ctypes.POINTER(i)]
+    lib.sift_hip_wait.argtypes = [vp, i, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    lib.sift_hip_fetch.argtypes = [vp, i, vp, vp]
+    lib.sift_hip_detect_batch.argtypes = [vp, ctypes.POINTER(vp), i, i, i, i, i,
+                                          ctypes.POINTER(CParams), ctypes.POINTER(vp),
+                                          ctypes.POINTER(sz), ctypes.POINTER(vp)]
     match_args = [vp, vp, sz, vp, sz, ctypes.c_double, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     lib.sift_hip_match.argtypes = match_args
     lib.sift_hip_match_device.argtypes = match_args
@@ -211,6 +227,7 @@ class Context:
         self._ctx = ctypes.c_void_p()
         _check(self.lib.sift_hip_create(device, ctypes.byref(self._ctx)))
         self.device = device
+        self._jobs = {}
 
     def close(self) -> None:
         if self._ctx:
@@ -223,41 +240,84 @@ class Context:
         except Exception:
             pass
 
-    def _finish(self, kp_ptr, n, df_ptr, want_f32):
-        n = n.value
+    # ---- jobs (submit / wait / fetch): batches of same-shape images, up to
+    # MAX_INFLIGHT in flight; results land directly in numpy storage
+    def submit(self, images, kind: int, w: int, h: int, c: int = 1,
+               params: SiftParams | None = None, desc_f32: bool = False) -> int:
+        """Enqueue one job: `images` is a sequence of host arrays (kind *_HOST)
+        or device pointers (kind *_DEVICE) of one shape. Host arrays must stay
+        alive until wait(); returns the ticket."""
+        n = len(images)
+        ptrs = (ctypes.c_void_p * n)()
+        for b, im in enumerate(images):
+            ptrs[b] = im if isinstance(im, int) else im.ctypes.data
+        p = (params or SiftParams()).to_c()
+        t = ctypes.c_int()
+        _check(self.lib.sift_hip_submit(self._ctx, ptrs, n, kind, w, h, c, ctypes.byref(p),
+                                        1 if desc_f32 else 0, ctypes.byref(t)))
+        self._jobs[t.value] = (n, desc_f32, images)
+        return t.value
+
+    def wait(self, ticket: int):
+        """Per-image keypoint counts of a submitted job (blocks until done)."""
+        n, _, _ = self._jobs[ticket]
+        counts = (ctypes.c_size_t * n)()
+        total = ctypes.c_size_t()
+        _check(self.lib.sift_hip_wait(self._ctx, ticket, counts, ctypes.byref(total)))
+        return list(counts)
+
+    def fetch(self, ticket: int):
+        """(list of per-image keypoint arrays, list of per-image descriptor
+        float arrays or None); releases the job."""
+        n, want_f32, _ = self._jobs[ticket]
+        counts = self.wait(ticket)
+        total = sum(counts)
+        kps = np.empty(total, dtype=KP_DTYPE)
+        df = np.empty((total, 128), dtype=np.float32) if want_f32 else None
         try:
-            kps = np.ctypeslib.as_array((ctypes.c_uint8 * (n * 168)).from_address(kp_ptr.value)) \
-                .view(KP_DTYPE).copy() if n else np.zeros(0, dtype=KP_DTYPE)
-            df = None
-            if want_f32:
-                df = np.frombuffer(ctypes.string_at(df_ptr.value, n * 512), dtype="<f4") \
-                    .reshape(n, 128).copy() if n else np.zeros((0, 128), np.float32)
+            _check(self.lib.sift_hip_fetch(self._ctx, ticket,
+                                           kps.ctypes.data if total else None,
+                                           df.ctypes.data if (want_f32 and total) else None))
         finally:
-            self.lib.sift_hip_free(kp_ptr)
-            if want_f32:
-                self.lib.sift_hip_free(df_ptr)
-        return kps, df
+            del self._jobs[ticket]
+        offs = np.cumsum([0] + counts)
+        k = [kps[offs[b]:offs[b + 1]] for b in range(n)]
+        d = [df[offs[b]:offs[b + 1]] for b in range(n)] if want_f32 else None
+        return k, d
 
     def detect(self, img: np.ndarray, params: SiftParams | None = None, desc_f32: bool = False):
         """detect_keypoints_and_descriptors on a host image (H,W[,C] float64)."""
         a, w, h, c = _as_hwc(img)
-        p = (params or SiftParams()).to_c()
-        kp_ptr, n, df_ptr = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p()
-        _check(self.lib.sift_hip_detect(self._ctx, a.ctypes.data, w, h, c, ctypes.byref(p),
-                                        ctypes.byref(kp_ptr), ctypes.byref(n),
-                                        ctypes.byref(df_ptr) if desc_f32 else None))
-        return self._finish(kp_ptr, n, df_ptr, desc_f32)
+        k, d = self.fetch(self.submit([a], INPUT_F64_HOST, w, h, c, params, desc_f32))
+        return k[0], (d[0] if desc_f32 else None)
+
+    def detect_u8(self, img: np.ndarray, params: SiftParams | None = None,
+                  desc_f32: bool = False):
+        """Same from the 8-bit pixels stb decodes (H,W[,C] uint8)."""
+        a = np.ascontiguousarray(img, dtype=np.uint8)
+        h, w = a.shape[:2]
+        c = 1 if a.ndim == 2 else a.shape[2]
+        k, d = self.fetch(self.submit([a], INPUT_U8_HOST, w, h, c, params, desc_f32))
+        return k[0], (d[0] if desc_f32 else None)
 
     def detect_device(self, dev_ptr: int, w: int, h: int, c: int = 1,
                       params: SiftParams | None = None, desc_f32: bool = False):
         """Same, with the image already resident in HBM (device pointer)."""
-        p = (params or SiftParams()).to_c()
-        kp_ptr, n, df_ptr = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p()
-        _check(self.lib.sift_hip_detect_device(self._ctx, ctypes.c_void_p(dev_ptr), w, h, c,
-                                               ctypes.byref(p), ctypes.byref(kp_ptr),
-                                               ctypes.byref(n),
-                                               ctypes.byref(df_ptr) if desc_f32 else None))
-        return self._finish(kp_ptr, n, df_ptr, desc_f32)
+        k, d = self.fetch(self.submit([int(dev_ptr)], INPUT_F64_DEVICE, w, h, c, params,
+                                      desc_f32))
+        return k[0], (d[0] if desc_f32 else None)
+
+    def detect_batch(self, images, params: SiftParams | None = None, desc_f32: bool = False,
+                     kind: int | None = None, shape=None):
+        """One job over several same-shape images (host arrays, or device
+        pointers with kind=INPUT_*_DEVICE and shape=(w, h, c)); lists of
+        per-image results."""
+        if kind is None:
+            arrs = [_as_hwc(im)[0] for im in images]
+            _, w, h, c = _as_hwc(arrs[0])
+            return self.fetch(self.submit(arrs, INPUT_F64_HOST, w, h, c, params, desc_f32))
+        w, h, c = shape
+        return self.fetch(self.submit([int(x) for x in images], kind, w, h, c, params, desc_f32))
 
     def _match_result(self, out, n):
         try:

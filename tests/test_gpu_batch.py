@@ -1,0 +1,185 @@
+"""GPU: jobs of several images (one batched launch per kernel), pipelined
+submits, the u8 upload path and the world-size-1 record exchange — each
+image's result against the oracle (the reference restated, pinned by the
+goldens) or the reference-generated 1080p golden.
+
+Reference: detect_keypoints_and_descriptors is a pure function of one image
+(src/sift.cpp:712-776), so every image of a job must come out exactly as if
+detected alone. Tolerances as tests/parity.py.
+"""
+import os
+import socket
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from golden_util import all_goldens
+from oracle_bind import OracleRun
+from parity import compare_final, final_ok
+from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, INPUT_U8_DEVICE, Context, SiftParams,
+                      synth_image)
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_finals(imgs, params=None):
+    # ctypes releases the GIL: the oracle runs of a batch go in parallel
+    def one(img):
+        r = OracleRun(img, params)
+        out = (r.final, r.desc_f32)
+        r.close()
+        return out
+
+    with ThreadPoolExecutor(max_workers=min(8, len(imgs))) as ex:
+        return list(ex.map(one, imgs))
+
+
+def _assert_same_records(a, b):
+    assert a.tobytes() == b.tobytes()
+
+
+def test_gpu_batch_small_vs_oracle(gpu_ctx):
+    imgs = [synth_image(320, 240, 1, seed=42 + i) for i in range(8)]
+    kps, dfs = gpu_ctx.detect_batch(imgs, desc_f32=True)
+    refs = _oracle_finals(imgs)
+    for b, (k, d, (rk, rd)) in enumerate(zip(kps, dfs, refs)):
+        r = compare_final(k, d, rk, rd)
+        assert final_ok(r), (b, r)
+    # a batch is the same as the images one at a time
+    for b in (0, 5):
+        k1, _ = gpu_ctx.detect(imgs[b])
+        _assert_same_records(kps[b], k1)
+
+
+def test_gpu_batch_rgb_params_vs_oracle(gpu_ctx):
+    p = SiftParams(double_image_size=False, intervals=4)
+    imgs = [synth_image(203, 151, 3, seed=7 + i) for i in range(3)]
+    kps, dfs = gpu_ctx.detect_batch(imgs, p, desc_f32=True)
+    for b, (k, d, (rk, rd)) in enumerate(zip(kps, dfs, _oracle_finals(imgs, p))):
+        assert final_ok(compare_final(k, d, rk, rd)), b
+
+
+def test_gpu_batch_identical_images_dedup_per_image(gpu_ctx):
+    # unique (sift.hh:25-27) must never merge records of different images
+    img = synth_image(200, 150, 1, seed=9)
+    kps, _ = gpu_ctx.detect_batch([img, img, img])
+    one, _ = gpu_ctx.detect(img)
+    for k in kps:
+        _assert_same_records(k, one)
+
+
+def test_gpu_batch8_1080p_vs_golden_and_oracle(gpu_ctx):
+    """BASELINE config 4 layout on one GPU: 8 1080p images in one job; seed 42
+    against the reference-generated golden, every image against the oracle."""
+    g = [x for x in all_goldens(kinds=("medium",)) if x.name == "synth_1920x1080"][0]
+    imgs = [g.input()] + [synth_image(1920, 1080, 1, seed=43 + i) for i in range(7)]
+    kps, dfs = gpu_ctx.detect_batch(imgs, desc_f32=True)
+    r = compare_final(kps[0], dfs[0], g.final, g.desc_f32)
+    assert final_ok(r) and len(kps[0]) == g.meta["final"], r
+    refs = _oracle_finals(imgs)
+    for b, (k, d, (rk, rd)) in enumerate(zip(kps, dfs, refs)):
+        r = compare_final(k, d, rk, rd)
+        assert final_ok(r), (b, r)
+
+
+def test_gpu_pipelined_jobs(gpu_ctx):
+    """Two jobs in flight; a third submit is refused; out-of-order waits."""
+    a = [synth_image(640, 480, 1, seed=s) for s in (1, 2)]
+    b = [synth_image(320, 240, 3, seed=3)]
+    wa, ha = 640, 480
+    ta = gpu_ctx.submit(a, INPUT_F64_HOST, wa, ha, 1)
+    tb = gpu_ctx.submit(b, INPUT_F64_HOST, 320, 240, 3)
+    with pytest.raises(RuntimeError, match="in flight"):
+        gpu_ctx.submit(b, INPUT_F64_HOST, 320, 240, 3)
+    kb, _ = gpu_ctx.fetch(tb)
+    ka, _ = gpu_ctx.fetch(ta)
+    _assert_same_records(ka[1], gpu_ctx.detect(a[1])[0])
+    _assert_same_records(kb[0], gpu_ctx.detect(b[0])[0])
+    # a steady stream: submit k+1 before fetching k
+    imgs = [synth_image(480, 360, 1, seed=100 + i) for i in range(5)]
+    solo = [gpu_ctx.detect(im)[0] for im in imgs]
+    t = gpu_ctx.submit([imgs[0]], INPUT_F64_HOST, 480, 360, 1)
+    for i in range(1, 6):
+        t_next = gpu_ctx.submit([imgs[i]], INPUT_F64_HOST, 480, 360, 1) if i < 5 else None
+        k, _ = gpu_ctx.fetch(t)
+        _assert_same_records(k[0], solo[i - 1])
+        t = t_next
+
+
+def test_gpu_u8_and_device_inputs(gpu_ctx):
+    import torch
+
+    img = synth_image(400, 300, 3, seed=21)
+    k64, d64 = gpu_ctx.detect(img, desc_f32=True)
+    k8, d8 = gpu_ctx.detect_u8(img.astype(np.uint8), desc_f32=True)
+    _assert_same_records(k64, k8)
+    assert np.array_equal(d64, d8)
+    t8 = torch.from_numpy(img.astype(np.uint8)).to("cuda:0")
+    t64 = torch.from_numpy(img).to("cuda:0")
+    torch.cuda.synchronize()
+    kd, _ = gpu_ctx.detect_batch([t8.data_ptr(), t8.data_ptr()], kind=INPUT_U8_DEVICE,
+                                 shape=(400, 300, 3))
+    _assert_same_records(kd[0], k64)
+    _assert_same_records(kd[1], k64)
+    kd, _ = gpu_ctx.detect_batch([t64.data_ptr(), t64.data_ptr()], kind=INPUT_F64_DEVICE,
+                                 shape=(400, 300, 3))
+    _assert_same_records(kd[1], k64)
+    # a non-integer image takes the double upload and still matches the oracle
+    frac = synth_image(160, 120, 1, seed=5) + 0.25
+    k, d = gpu_ctx.detect(frac, desc_f32=True)
+    ref = OracleRun(frac)
+    assert final_ok(compare_final(k, d, ref.final, ref.desc_f32))
+
+
+def test_gpu_small_batch_threshold_keeps_every_octave():
+    """with SIFT_BATCH_PX_LOG2 small, octaves built only by the
+    LDS kernel must still be searched (final batch starts at o_small)."""
+    os.environ["SIFT_BATCH_PX_LOG2"] = "10"
+    try:
+        ctx = Context(0)
+    finally:
+        del os.environ["SIFT_BATCH_PX_LOG2"]
+    try:
+        img = synth_image(640, 360, 1, seed=42)
+        k, d = ctx.detect(img, desc_f32=True)
+        ref = OracleRun(img)
+        assert final_ok(compare_final(k, d, ref.final, ref.desc_f32))
+    finally:
+        ctx.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_gpu_batch_record_exchange_world1(gpu_ctx):
+    """The config-4 data path at world size 1 over RCCL: a batch through HIP,
+    its records through allgather_records and the pipelined RecordExchange."""
+    import torch
+    import torch.distributed as dist
+
+    from sift_dist import RECORD_BYTES, RecordExchange, allgather_records
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        dev = torch.device("cuda", 0)
+        imgs = [synth_image(480, 360, 1, seed=300 + i) for i in range(4)]
+        kps, _ = gpu_ctx.detect_batch(imgs)
+        ids = list(range(4))
+        bufs = [torch.from_numpy(k.view(np.uint8).reshape(-1, RECORD_BYTES).copy()) for k in kps]
+        got = allgather_records([b.to(dev) for b in bufs], ids, 4)
+        for i in ids:
+            assert got[i].cpu().numpy().tobytes() == kps[i].tobytes()
+        ex = RecordExchange(4096, dev)
+        s = ex.push(bufs, ids)
+        ex.flush()
+        res = ex.result(s)
+        for i in ids:
+            assert res[i].cpu().numpy().tobytes() == kps[i].tobytes()
+    finally:
+        dist.destroy_process_group()
