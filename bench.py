@@ -186,6 +186,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-matcher", action="store_true",
                     help="skip the matcher measurement (SURVEY §8f row 1)")
+    ap.add_argument("--sync", action="store_true",
+                    help="one job at a time (no pipelining), for profiling / A-B")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the latency / API / batch8 legs")
     ap.add_argument("--extra-seconds", type=float, default=2.0)
@@ -246,6 +248,10 @@ def main() -> int:
 
     def run(n_steps: int) -> int:
         kp = 0
+        if args.sync:
+            for _ in range(n_steps):
+                kp += finish(submit())
+            return kp
         t = submit()
         for k in range(n_steps):
             t_next = submit() if k + 1 < n_steps else None

@@ -17,10 +17,17 @@
 //
 // usage: ref_harness <input> <out_prefix> [intervals=3] [double=1]
 //                    [max_octaves=0] [dump_pyramid=0]
+//                    [window_size=3] [init_sigma=1.6] [contrast_threshold=0.04]
+//                    [eigen_ratio=10] [num_bins=36] [peak_ratio=0.8]
+//                    [ori_sigma_factor=1.5] [desc_scale_factor=3]
 //        ref_harness --match <kps1.bin> <kps2.bin> <ratio> <out.bin>
+//   (the trailing arguments are the remaining parameters of
+//   detect_keypoints_and_descriptors, reference sift.hh:65-71, parsed with
+//   strtod so every double round-trips exactly from its repr)
 //   <input> is an image file (stb decode, image_io.cpp:20-35) or a raw file
 //   "SIFTRAW1" + int32 w,h,c + w*h*c little-endian doubles.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <string>
@@ -111,10 +118,12 @@ int main(int argc, char** argv) {
     const bool dbl = argc > 4 ? std::atoi(argv[4]) != 0 : true;
     const int max_oct = argc > 5 ? std::atoi(argv[5]) : 0;
     const bool dump_pyr = argc > 6 ? std::atoi(argv[6]) != 0 : false;
-    // reference defaults, sift.hh:65-71
-    const double init_sigma = 1.6, ct = 0.04, er = 10.0, num_bins = 36,
-                 peak_ratio = 0.8, ori_sf = 1.5, desc_sf = 3.0;
-    const int window_size = 3;
+    // reference defaults, sift.hh:65-71, unless given
+    auto dbl_arg = [&](int i, double d) { return argc > i ? std::strtod(argv[i], nullptr) : d; };
+    const int window_size = argc > 7 ? std::atoi(argv[7]) : 3;
+    const double init_sigma = dbl_arg(8, 1.6), ct = dbl_arg(9, 0.04), er = dbl_arg(10, 10.0),
+                 num_bins = dbl_arg(11, 36), peak_ratio = dbl_arg(12, 0.8),
+                 ori_sf = dbl_arg(13, 1.5), desc_sf = dbl_arg(14, 3.0);
 
     Image img;
     if (!read_raw(argv[1], img)) {

@@ -19,6 +19,16 @@
 // (wait / fetch): the device runs job k+1's pyramid while the host sorts job
 // k's records. Completion is tracked with per-slot events only — no stream
 // synchronisation on the pipelined path.
+//
+// Streams. HIP gives a process four hardware queues by default and streams
+// beyond that share a queue and serialise, so a context has exactly four:
+// slot s owns a pyramid stream (high priority) and a keypoint stream (low
+// priority). A job submitted while the other slot has work in flight uses
+// its own pair only, so two jobs never wait on each other (with shared
+// streams the pyramid chains of consecutive jobs serialised and set the
+// step time); a job submitted while the other slot is idle (synchronous use)
+// borrows the other pair too: octaves alternate between both pyramid
+// streams and keypoint batches between both keypoint streams.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -182,6 +192,11 @@ struct Slot {
     int n_chains = 0, ev_i = 0;
     size_t ev_used = 0;
     hipEvent_t done_ev = nullptr;  // lane counters on the host
+    // streams of the current job: A, B pyramid (even / odd octaves), C, D
+    // keypoint lanes 0 / 1 (A == B and C == D when the job runs alone on its
+    // slot's pair)
+    hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
+    int lanes = kLanes;
     std::vector<EventPair> pending;
     // finalize
     bool exported = true;
@@ -206,17 +221,20 @@ struct Slot {
 
 struct sift_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;   // A: pyramid (even octaves), public stream
-    hipStream_t stream2 = nullptr;  // B: odd octaves of the pyramid
-    hipStream_t stream3 = nullptr;  // C: keypoint chains of even batches (lane 0)
-    hipStream_t stream4 = nullptr;  // D: keypoint chains of odd batches (lane 1)
+    hipStream_t stream = nullptr;  // = pyr_stream[0]: the public stream (matcher)
     // persistent workgroups of orientation / descriptor per launch: 512 (two
     // per CU; with two keypoint lanes in flight this leaves room for the
     // small octaves' blurs); measured best of 256/384/512/768/1024
     unsigned kp_wgs = 512;
     int batch_px_log2 = 18;  // octaves of >= 2^this pixels (x images) get their own batch
+    size_t tile_max_px = (size_t)1 << 21;  // planes up to this size: LDS-tile blur
+    bool shared_streams = false;  // SIFT_SHARED_STREAMS=1: every job on all four streams
+    bool serial = false;          // SIFT_SERIAL=1: every kernel on one stream (profiling)
+    bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
+    hipStream_t pyr_stream[kSlots] = {};  // slot s: pyramid (high priority)
+    hipStream_t kp_stream[kSlots] = {};   // slot s: keypoint chains (low priority)
     int next_ticket = 1;
     int last = -1;  // slot of the last finalised job (introspection)
 
@@ -272,19 +290,36 @@ int prof_events(sift_ctx* ctx, Slot& s, hipEvent_t* e0, hipEvent_t* e1, double b
     return SIFT_OK;
 }
 
-ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end) {
+// task table of one extrema launch over octaves [o_begin, o_end): tiles of
+// 64 x 16 centres (k_extrema_tiles) or strips of kExtSpan columns x kExtSeg
+// rows (k_extrema_stream)
+ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img, bool stream) {
     ExtremaGrid eg;
     std::memset(&eg, 0, sizeof eg);
+    const int cw = stream ? kExtSpan : 64;
     for (int o = o_begin; o < o_end; ++o) {
         const int i = eg.n++;
-        const int tx = g.W[o] > 2 ? (g.W[o] - 2 + 63) / 64 : 0;
-        const int ty = g.H[o] > 2 ? (g.H[o] - 2 + 15) / 16 : 0;
+        const int tx = g.W[o] > 2 ? (g.W[o] - 2 + cw - 1) / cw : 0;
+        // streaming: segments short enough for ~4096 waves per octave over
+        // the job (the small octaves are latency-bound), at least 4 rows
+        // (2 priming rows per segment), at most 64
+        int ch = 16;
+        if (stream) {
+            const long rows = (long)tx * std::max(g.H[o] - 2, 0) * n_img / 4096;
+            ch = (int)std::min<long>(64, std::max<long>(4, rows));
+        }
+        const int ty = g.H[o] > 2 ? (g.H[o] - 2 + ch - 1) / ch : 0;
         eg.oct[i] = o;
         eg.tiles_x[i] = tx > 0 ? tx : 1;
+        eg.seg[i] = ch;
         eg.first_tile[i + 1] = eg.first_tile[i] + tx * ty;
     }
     return eg;
 }
+
+hipError_t launch_extrema_set(const sift_ctx* ctx, const PyrTable* d_pt, const Geometry& g,
+                              int o_begin, int o_end, int n_img, int thr, sift_extremum* cand,
+                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s);
 
 // keypoint-array capacities of a slot (per lane), all size_t and bounded so
 // that the kernels' 32-bit indices and the df32 product never wrap
@@ -304,10 +339,10 @@ int ensure_kp_arrays(Slot& s, size_t cand, size_t raw, size_t ori) {
 // After a failure with work already enqueued: let every stream drain before
 // the slot's buffers can be touched again, then free the slot.
 void abandon(sift_ctx* ctx, Slot& s) {
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipStreamSynchronize(ctx->stream2);
-    (void)hipStreamSynchronize(ctx->stream3);
-    (void)hipStreamSynchronize(ctx->stream4);
+    for (int k = 0; k < kSlots; ++k) {
+        (void)hipStreamSynchronize(ctx->pyr_stream[k]);
+        (void)hipStreamSynchronize(ctx->kp_stream[k]);
+    }
     s.pending.clear();
     s.state = kFree;
     s.ticket = -1;
@@ -329,7 +364,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     s.n_chains = 0;
     s.chain_lane.clear();
     int st;
-    hipStream_t sA = ctx->stream, sB = ctx->stream2, sC = ctx->stream3, sD = ctx->stream4;
+    hipStream_t sA = s.sA, sB = s.sB, sC = s.sC, sD = s.sD;
 
     // ---- input images -> device (contiguous, image b at src + b * in_bs)
     const size_t ne = (size_t)s.w * s.h * s.c;
@@ -412,7 +447,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                                std::max(s.cap_ori, 2 * want_cand))) != SIFT_OK)
         return st;
 
-    const int lanes = ctx->lanes;
+    const int lanes = s.lanes;
     hipStream_t lane_stream[kLanes] = {sC, sD};
     SIFT_HIP_TRY(hipMemsetAsync(s.d_ctr, 0, kCtrWords * sizeof(unsigned), sA));
 
@@ -428,7 +463,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         double* decp = dec ? s.h_pt.lvl[o + 1][0] : nullptr;
         double* tmp = wide ? s.tmp.p + (o & 1) * tmp_half : nullptr;
         SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp, so,
-                                 e0, e1));
+                                 e0, e1, ctx->tile_max_px));
         return SIFT_OK;
     };
 
@@ -530,9 +565,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                             s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
                             (unsigned)s.exp_lane};
         if (tiles) {
-            const ExtremaGrid eg = extrema_grid(g, o_begin, o_end);
-            SIFT_HIP_TRY(launch_extrema_tiles(d_pt, eg, n_img, g.n_gauss, dp.threshold, cand,
-                                              live + 0, cap_cand, begin, sx));
+            SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
+                                            cand, live + 0, cap_cand, begin, sx));
         } else {
             for (int o = o_begin; o < o_end; ++o)
                 SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], n_img, g.n_gauss,
@@ -632,7 +666,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     const Geometry& g = s.g;
     const sift_params* p = &s.p;
     int st;
-    hipStream_t sC = ctx->stream3;
+    hipStream_t sC = s.sC;
     s.exported = true;
     s.n_keys = 0;
     s.run_start.clear();
@@ -674,9 +708,9 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
                            cap_ori = (unsigned)s.cap_ori;
             const ExportSink ex{s.exp_rec.d, s.exp_side.d, nullptr, 0};
             if (tiles) {
-                const ExtremaGrid eg = extrema_grid(g, 0, g.octaves);
-                SIFT_HIP_TRY(launch_extrema_tiles(d_pt, eg, s.n_img, g.n_gauss, s.dp.threshold,
-                                                  s.cand.p, live, cap_cand, nullptr, sC));
+                SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, 0, g.octaves, s.n_img,
+                                                s.dp.threshold, s.cand.p, live, cap_cand, nullptr,
+                                                sC));
             } else {
                 for (int o = 0; o < g.octaves; ++o)
                     SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], s.n_img, g.n_gauss,
@@ -807,6 +841,15 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     return SIFT_OK;
 }
 
+hipError_t launch_extrema_set(const sift_ctx* ctx, const PyrTable* d_pt, const Geometry& g,
+                              int o_begin, int o_end, int n_img, int thr, sift_extremum* cand,
+                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s) {
+    const ExtremaGrid eg = extrema_grid(g, o_begin, o_end, n_img, ctx->extrema_stream);
+    return ctx->extrema_stream
+               ? launch_extrema_stream(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s)
+               : launch_extrema_tiles(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s);
+}
+
 Slot* slot_of(sift_ctx* ctx, int ticket) {
     for (Slot& s : ctx->slots)
         if (s.state != kFree && s.ticket == ticket) return &s;
@@ -848,6 +891,20 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     s.want_df = want_df != 0;
     s.ticket = ctx->next_ticket++;
     if (ctx->next_ticket <= 0) ctx->next_ticket = 1;
+    {
+        int me = (int)(&s - ctx->slots), other = 1 - me;
+        const bool alone = ctx->shared_streams || ctx->slots[other].state != kSubmitted;
+        if (ctx->shared_streams) me = 0, other = 1;  // A/B: every job on all four
+        s.sA = ctx->pyr_stream[me];
+        s.sC = ctx->kp_stream[me];
+        s.sB = alone ? ctx->pyr_stream[other] : s.sA;
+        s.sD = alone ? ctx->kp_stream[other] : s.sC;
+        s.lanes = alone ? ctx->lanes : 1;
+        if (ctx->serial) {  // profiling: one stream, no overlap (kernel costs alone)
+            s.sA = s.sB = s.sC = s.sD = ctx->pyr_stream[0];
+            s.lanes = 1;
+        }
+    }
     s.state = kSubmitted;
     st = enqueue_job(ctx, s, images, kind);
     if (st != SIFT_OK) {
@@ -917,15 +974,21 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) ctx->batch_px_log2 = std::atoi(e);
     if (const char* e = std::getenv("SIFT_KP_LANES")) ctx->lanes = std::atoi(e) == 1 ? 1 : kLanes;
     if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 18;
-    bool ok = hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) ==
-                  hipSuccess &&
-              hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) ==
-                  hipSuccess &&
-              hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_lo) ==
-                  hipSuccess &&
-              hipStreamCreateWithPriority(&ctx->stream4, hipStreamNonBlocking, prio_lo) ==
-                  hipSuccess &&
-              prepare_kernel_attributes() == hipSuccess;
+    if (const char* e = std::getenv("SIFT_SHARED_STREAMS")) ctx->shared_streams = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_EXTREMA_TILES")) ctx->extrema_stream = std::atoi(e) == 0;
+    if (const char* e = std::getenv("SIFT_TILE_PX_LOG2")) {
+        const int t = std::atoi(e);  // < 0: never
+        ctx->tile_max_px = t < 0 ? 0 : (size_t)1 << std::min(t, 40);
+    }
+    bool ok = prepare_kernel_attributes() == hipSuccess;
+    for (int k = 0; k < kSlots; ++k)
+        ok = ok &&
+             hipStreamCreateWithPriority(&ctx->pyr_stream[k], hipStreamNonBlocking, prio_hi) ==
+                 hipSuccess &&
+             hipStreamCreateWithPriority(&ctx->kp_stream[k], hipStreamNonBlocking, prio_lo) ==
+                 hipSuccess;
+    ctx->stream = ctx->pyr_stream[0];
     for (Slot& s : ctx->slots) {
         ok = ok && hipMalloc(&s.d_ctr, kCtrWords * sizeof(unsigned)) == hipSuccess &&
              hipHostMalloc(&s.h_ctr, 4 * kLanes * sizeof(unsigned)) == hipSuccess &&
@@ -944,8 +1007,10 @@ int sift_hip_create(int device, sift_ctx** out) {
 int sift_hip_destroy(sift_ctx* ctx) {
     if (!ctx) return SIFT_ERR_ARG;
     (void)hipSetDevice(ctx->device);
-    for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4})
-        if (st) (void)hipStreamSynchronize(st);
+    for (int k = 0; k < kSlots; ++k) {
+        if (ctx->pyr_stream[k]) (void)hipStreamSynchronize(ctx->pyr_stream[k]);
+        if (ctx->kp_stream[k]) (void)hipStreamSynchronize(ctx->kp_stream[k]);
+    }
     for (Slot& s : ctx->slots) {
         s.in.release();
         s.in8.release();
@@ -975,8 +1040,10 @@ int sift_hip_destroy(sift_ctx* ctx) {
     if (ctx->d_mbuf) (void)hipFree(ctx->d_mbuf);
     ctx->h_mj.release();
     ctx->h_md.release();
-    for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4})
-        if (st) (void)hipStreamDestroy(st);
+    for (int k = 0; k < kSlots; ++k) {
+        if (ctx->pyr_stream[k]) (void)hipStreamDestroy(ctx->pyr_stream[k]);
+        if (ctx->kp_stream[k]) (void)hipStreamDestroy(ctx->kp_stream[k]);
+    }
     delete ctx;
     return SIFT_OK;
 }
@@ -1189,9 +1256,8 @@ int sift_hip_copy_level(sift_ctx* ctx, int octave, int level, double* host_out,
     if (cap_elems < (size_t)W * H) return SIFT_ERR_ARG;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
     SIFT_HIP_TRY(hipMemcpyAsync(host_out, s->h_pt.lvl[octave][level],
-                                (size_t)W * H * sizeof(double), hipMemcpyDeviceToHost,
-                                ctx->stream));
-    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+                                (size_t)W * H * sizeof(double), hipMemcpyDeviceToHost, s->sA));
+    SIFT_HIP_TRY(hipStreamSynchronize(s->sA));
     if (w_out) *w_out = W;
     if (h_out) *h_out = H;
     return SIFT_OK;
@@ -1210,8 +1276,8 @@ int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out, size_t cap, si
         if (s->lane_n[0][L])
             SIFT_HIP_TRY(hipMemcpyAsync(host_out + off, s->cand.p + (size_t)L * s->cap_cand,
                                         s->lane_n[0][L] * sizeof(sift_extremum),
-                                        hipMemcpyDeviceToHost, ctx->stream));
-    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+                                        hipMemcpyDeviceToHost, s->sA));
+    SIFT_HIP_TRY(hipStreamSynchronize(s->sA));
     return SIFT_OK;
 }
 
@@ -1229,8 +1295,8 @@ int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t*
             SIFT_HIP_TRY(hipMemcpyAsync(static_cast<sift_kp*>(d_dst) + off,
                                         s->ori.p + (size_t)L * s->cap_ori,
                                         s->lane_n[2][L] * sizeof(sift_kp),
-                                        hipMemcpyDeviceToDevice, ctx->stream));
-    SIFT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+                                        hipMemcpyDeviceToDevice, s->sA));
+    SIFT_HIP_TRY(hipStreamSynchronize(s->sA));
     return SIFT_OK;
 }
 

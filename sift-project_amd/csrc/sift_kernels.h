@@ -24,9 +24,11 @@ hipError_t launch_prepare(const double* in, size_t in_bs, int w, int h, int c, i
                           double* out, size_t out_bs, int W0, int H0, int n_img, hipStream_t s);
 // e0/e1: optional HIP events timestamped by the dispatch itself (profiling);
 // tmp: n_img * W * H doubles for kernels wider than kMaxTemplR
+// planes of at most tile_max_px pixels use the LDS-tile kernel (k_blur_tile),
+// larger ones the strip walk (k_blur)
 hipError_t launch_blur(const double* src, size_t src_bs, double* dst, size_t bs, int n_img, int W,
                        int H, const BlurTaps& taps, double* dec, int Wd, int Hd, double* tmp,
-                       hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+                       hipStream_t s, hipEvent_t e0, hipEvent_t e1, size_t tile_max_px);
 // Initial blur fused with gray/bilinear-x2 staging from the input images
 // (image b at in + b * in_bs). Returns false (nothing launched) when the
 // fused path does not apply.
@@ -44,6 +46,10 @@ hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int
 hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
                                 int n_gauss, int thr, sift_extremum* out, unsigned* counter,
                                 unsigned cap, unsigned* snap, hipStream_t s);
+// streaming variant (window_size 3): eg tasks = strips x segments per octave
+hipError_t launch_extrema_stream(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
+                                 int n_gauss, int thr, sift_extremum* out, unsigned* counter,
+                                 unsigned cap, unsigned* snap, hipStream_t s);
 hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_img, int n_gauss,
                               int window_size, int thr, sift_extremum* out, unsigned* counter,
                               unsigned cap, hipStream_t s);

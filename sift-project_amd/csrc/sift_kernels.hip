@@ -285,6 +285,111 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// k_blur_tile<R, DECIM>: the same level (image.cpp:156-214) for planes small
+// enough to be cache-resident (octaves >= 1 of a 1080p image), where the
+// strip walk of k_blur is latency-bound (2R+1+rows serial steps per wave).
+// One workgroup per 64 x 32 output tile: the (32+2R) x (64+2R) source
+// region (replicate border by clamping) is staged in LDS with one round of
+// loads, the row pass writes (32+2R) x 64 row-pass values to LDS, the column
+// pass produces the tile. Each thread evaluates runs of outputs (4 along x in
+// the row pass, 8 along y in the column pass) from one register window, so
+// an output costs ~(run+2R)/run LDS reads instead of 2R+1. Same arithmetic
+// and order as k_blur per output (acc = v*k0, acc += k[u]*(v[+u]+v[-u]),
+// Markstein-corrected division by sum_w), hence bit-identical planes. LDS
+// row strides are odd in doubles so lane-per-row accesses are conflict-free.
+// ---------------------------------------------------------------------------
+constexpr int kTileW = 64, kTileH = 32;
+
+template <int R, bool DECIM>
+__global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ src, size_t src_bs,
+                                                   double* __restrict__ dst, size_t bs, int W,
+                                                   int H, BlurTaps taps,
+                                                   double* __restrict__ dec, int Wd, int Hd) {
+    constexpr int SH = kTileH + 2 * R;             // staged rows
+    constexpr int SWp = (kTileW + 2 * R) | 1;      // staged row stride (odd)
+    constexpr int TWp = kTileW + 1;                // row-pass row stride (odd)
+    constexpr int RX = 4, RY = 8;                  // output runs per task
+    __shared__ double sin_[SH * SWp];
+    __shared__ double tmp[SH * TWp];
+    const int tid = threadIdx.x;
+    int bx, by, bz;
+    xcd_remap(bx, by, bz);
+    gdouble* g = gbl(src + bz * src_bs);
+    dst += bz * bs;
+    if (DECIM) dec += bz * bs;
+    const int x0 = bx * kTileW, y0 = by * kTileH;
+    double k[R + 1];
+#pragma unroll
+    for (int u = 0; u <= R; ++u) k[u] = taps.k[u];
+    const double sw = taps.sum_w, inv = taps.inv;
+    // stage: all loads of a thread in flight before the LDS stores
+    {
+        constexpr int N = SH * (kTileW + 2 * R);
+        constexpr int NIT = (N + 255) / 256;
+        double v[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int i = tid + 256 * it;
+            const int r = i / (kTileW + 2 * R), c = i - r * (kTileW + 2 * R);
+            const int gy = clampi(y0 - R + r, 0, H - 1), gx = clampi(x0 - R + c, 0, W - 1);
+            v[it] = (i < N) ? g[(size_t)gy * W + gx] : 0.0;
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int i = tid + 256 * it;
+            const int r = i / (kTileW + 2 * R), c = i - r * (kTileW + 2 * R);
+            if (i < N) sin_[r * SWp + c] = v[it];
+        }
+    }
+    __syncthreads();
+    // row pass (image.cpp:170-185): task = (row r, columns c0..c0+RX-1);
+    // consecutive lanes take consecutive rows
+    for (int t = tid; t < SH * (kTileW / RX); t += 256) {
+        const int r = t % SH, c0 = (t / SH) * RX;
+        const double* row = sin_ + r * SWp + c0;
+        double v[RX + 2 * R];
+#pragma unroll
+        for (int j = 0; j < RX + 2 * R; ++j) v[j] = row[j];
+        double acc[RX];
+#pragma unroll
+        for (int j = 0; j < RX; ++j) acc[j] = v[j + R] * k[0];
+#pragma unroll
+        for (int u = 1; u <= R; ++u)
+#pragma unroll
+            for (int j = 0; j < RX; ++j) acc[j] += k[u] * (v[j + R + u] + v[j + R - u]);
+#pragma unroll
+        for (int j = 0; j < RX; ++j) tmp[r * TWp + c0 + j] = div_sum_w(acc[j], sw, inv);
+    }
+    __syncthreads();
+    // column pass (image.cpp:193-208): task = (column c, rows r0..r0+RY-1)
+    {
+        const int c = tid % kTileW, r0 = (tid / kTileW) * RY;
+        double v[RY + 2 * R];
+#pragma unroll
+        for (int j = 0; j < RY + 2 * R; ++j) v[j] = tmp[(r0 + j) * TWp + c];
+        double acc[RY];
+#pragma unroll
+        for (int j = 0; j < RY; ++j) acc[j] = v[j + R] * k[0];
+#pragma unroll
+        for (int u = 1; u <= R; ++u)
+#pragma unroll
+            for (int j = 0; j < RY; ++j) acc[j] += k[u] * (v[j + R + u] + v[j + R - u]);
+        const int x = x0 + c;
+#pragma unroll
+        for (int j = 0; j < RY; ++j) {
+            const int y = y0 + r0 + j;
+            if (x < W && y < H) {
+                const double o = div_sum_w(acc[j], sw, inv);
+                dst[(size_t)y * W + x] = o;
+                if (DECIM && !(x & 1) && !(y & 1) && (x >> 1) < Wd && (y >> 1) < Hd)
+                    dec[(size_t)(y >> 1) * Wd + (x >> 1)] = o;
+            }
+        }
+    }
+}
+static_assert(kTileH == 4 * 8, "column pass: 256 threads = 64 columns x 4 runs of 8 rows");
+
+// ---------------------------------------------------------------------------
 // k_octaves_lds: every remaining small octave (W*H <= kLdsOctavePx) in ONE
 // launch of ONE workgroup. A level and the horizontal-pass temporary both
 // live in LDS, so each level is two barrier-separated LDS sweeps instead of
@@ -628,6 +733,162 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
     snapshot_if_last(snap, counter);
 }
 
+// ---------------------------------------------------------------------------
+// k_extrema_stream<NL>: the same test (sift.cpp:227-291, window_size 3) as a
+// streaming scan. One wavefront per task = (octave, strip of 62 centre
+// columns, segment of centre rows); lane l owns column x0 - 1 + l
+// (lanes 0 and 63 are the halo). The wave walks the rows of its segment:
+// per row every lane loads the NL Gaussian levels of its column (PF rows in
+// flight), forms the NL-1 DoG values, gets its x-1 / x+1 neighbours with DPP
+// wave shifts (no LDS), and keeps the 3-row window of horizontal max / min
+// of every layer in registers (ring slots are compile-time: the row loop is
+// unrolled by 3). Row y's centres are decided when row y+1 arrives; the
+// cube of DoG layer z is layers z-1..z+1, rows y-1..y+1, columns x-1..x+1,
+// and the test is the reference's non-strict one (v is in its own cube, so
+// "no neighbour greater" == (v == max)). No LDS, no barrier until the end;
+// 48 B read per pixel and (62 + 2) / 62 x (kExtSeg + 2) / kExtSeg reuse.
+// Candidates: ballot per (row, layer) into a per-wave LDS buffer, one
+// counter atomic per wave. The last workgroup takes the lane snapshot as
+// k_extrema_tiles does.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double dpp_from_left(double v) {  // lane i <- lane i-1
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_from_right(double v) {  // lane i <- lane i+1
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+template <int NL>
+__global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restrict__ pt,
+                                                        ExtremaGrid eg, int thr,
+                                                        sift_extremum* __restrict__ out,
+                                                        unsigned* __restrict__ counter,
+                                                        unsigned cap, unsigned* snap) {
+    constexpr int ND = NL - 1;   // DoG layers
+    constexpr int NZ = ND - 2;   // layers with a full cube (z = 1 .. ND-2)
+    constexpr int PF = 2;        // rows in flight
+    constexpr unsigned kCandBuf = 256;  // per-wave candidate buffer (LDS)
+    __shared__ sift_extremum cbuf[4][kCandBuf];
+    const int lane = threadIdx.x & 63;
+    const int task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int b = blockIdx.y;
+    if (task < eg.first_tile[eg.n]) {
+        int e = 0;
+        while (e + 1 < eg.n && task >= eg.first_tile[e + 1]) ++e;
+        const int o = eg.oct[e];
+        const int t = task - eg.first_tile[e];
+        const int strip = t % eg.tiles_x[e], seg = t / eg.tiles_x[e];
+        const int W = pt->w[o], H = pt->h[o];
+        const int xc0 = 1 + strip * kExtSpan;  // first centre column of the strip
+        const int x = xc0 - 1 + lane;
+        const int gx = min(x, W - 1);
+        const bool centre_lane = lane >= 1 && lane <= kExtSpan && x <= W - 2;
+        const int yc0 = 1 + seg * eg.seg[e];
+        const int yc1 = min(yc0 + eg.seg[e], H - 1);  // centres [yc0, yc1)
+        const int r0 = yc0 - 1, r1 = yc1;           // rows read, inclusive
+        gdouble* lv[NL];
+#pragma unroll
+        for (int l = 0; l < NL; ++l) lv[l] = gbl(plane(pt, b, o, l)) + gx;
+        const double dthr = (double)thr;
+        const int otag = o | (b << kOctBits);
+        // candidates collect in a per-wave LDS buffer and go out with ONE
+        // counter atomic per wave (per full buffer): a returning atomic per
+        // (row, layer) on the single global counter serialised the whole
+        // launch on the small octaves, where candidates are dense
+        sift_extremum* cb = cbuf[threadIdx.x >> 6];
+        unsigned nbuf = 0;  // wave-uniform
+        auto flush = [&]() {
+            if (nbuf == 0) return;
+            wave_sync();
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(counter, nbuf);
+            base = __shfl(base, 0);
+            for (unsigned i = lane; i < nbuf; i += 64)
+                if (base + i < cap) out[base + i] = cb[i];
+            wave_sync();
+            nbuf = 0;
+        };
+        double pf[PF][NL];
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const size_t ro = (size_t)min(r0 + p, r1) * W;
+#pragma unroll
+            for (int l = 0; l < NL; ++l) pf[p][l] = lv[l][ro];
+        }
+        double hmx[3][ND], hmn[3][ND], dc[3][NZ];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int z = 0; z < ND; ++z) hmx[q][z] = hmn[q][z] = 0.0;
+        for (int rb = r0; rb <= r1; rb += 3) {
+#pragma unroll
+            for (int sl = 0; sl < 3; ++sl) {
+                const int r = rb + sl;
+                if (r <= r1) {
+                    double g[NL];
+#pragma unroll
+                    for (int l = 0; l < NL; ++l) g[l] = pf[0][l];
+#pragma unroll
+                    for (int p = 0; p + 1 < PF; ++p)
+#pragma unroll
+                        for (int l = 0; l < NL; ++l) pf[p][l] = pf[p + 1][l];
+                    {
+                        const size_t ro = (size_t)min(r + PF, r1) * W;
+#pragma unroll
+                        for (int l = 0; l < NL; ++l) pf[PF - 1][l] = lv[l][ro];
+                    }
+                    // row r: DoG, horizontal 3-max / 3-min per layer
+#pragma unroll
+                    for (int z = 0; z < ND; ++z) {
+                        const double d = g[z + 1] - g[z];
+                        const double dl = dpp_from_left(d), dr = dpp_from_right(d);
+                        hmx[sl][z] = fmax(fmax(dl, d), dr);
+                        hmn[sl][z] = fmin(fmin(dl, d), dr);
+                        if (z >= 1 && z <= NZ) dc[sl][z - 1] = d;
+                    }
+                    // centres of row y = r - 1 (slot sl+2), rows y-1 / y+1 in
+                    // slots sl+1 / sl
+                    if (r >= r0 + 2) {
+                        const int y = r - 1;
+                        const int sy = (sl + 2) % 3, sp = (sl + 1) % 3;  // unrolled: constants
+#pragma unroll
+                        for (int z = 1; z <= NZ; ++z) {
+                            const double v = dc[sy][z - 1];
+                            bool cand = false;
+                            if (centre_lane && fabs(v) > dthr) {
+                                double mx = hmx[sy][z], mn = hmn[sy][z];
+#pragma unroll
+                                for (int dz = -1; dz <= 1; ++dz) {
+                                    mx = fmax(mx, fmax(fmax(hmx[sp][z + dz], hmx[sy][z + dz]),
+                                                       hmx[sl][z + dz]));
+                                    mn = fmin(mn, fmin(fmin(hmn[sp][z + dz], hmn[sy][z + dz]),
+                                                       hmn[sl][z + dz]));
+                                }
+                                cand = (v == mx) || (v == mn);
+                            }
+                            const unsigned long long m = __ballot(cand);
+                            if (m) {
+                                const unsigned k = (unsigned)__popcll(m);
+                                if (nbuf + k > kCandBuf) flush();
+                                if (cand)
+                                    cb[nbuf + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] =
+                                        sift_extremum{x, y, z, otag};
+                                nbuf += k;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        flush();
+    }
+    snapshot_if_last(snap, counter);
+}
+
 // Generic border b (window_size 4..7): one thread per (x, y), direct cube.
 __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict__ pt, int o,
                                                      int thr, int b, int nd,
@@ -749,14 +1010,28 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
                                                 unsigned cap_out) {
     const unsigned n = min(*n_cand, cap_cand);
     const unsigned i0 = min(*cand_begin, n);
-    for (unsigned i = i0 + blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += gridDim.x * blockDim.x) {
-        const sift_extremum e = cand[i];
+    // grid-stride over whole waves (wave-uniform trip count), so the kept
+    // keypoints of a wave take one counter atomic (ballot + prefix)
+    const int lane = threadIdx.x & 63;
+    const unsigned stride = gridDim.x * blockDim.x;
+    for (unsigned i0w = i0 + blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0w < n;
+         i0w += stride) {
+        const unsigned i = i0w + lane;
         RawKp r;
-        const int o = e.octave & ((1 << kOctBits) - 1), im = e.octave >> kOctBits;
-        if (!refine_one(pt, P, e.x, e.y, e.z, o, im, &r)) continue;
-        const unsigned idx = atomicAdd(n_out, 1u);
-        if (idx < cap_out) out[idx] = r;
+        bool keep = false;
+        if (i < n) {
+            const sift_extremum e = cand[i];
+            const int o = e.octave & ((1 << kOctBits) - 1), im = e.octave >> kOctBits;
+            keep = refine_one(pt, P, e.x, e.y, e.z, o, im, &r);
+        }
+        const unsigned long long m = __ballot(keep);
+        if (m) {
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(n_out, (unsigned)__popcll(m));
+            base = __shfl(base, 0);
+            const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            if (keep && idx < cap_out) out[idx] = r;
+        }
     }
 }
 
@@ -1279,10 +1554,34 @@ static hipError_t launch_blur_shaped(int MODE, const BlurSource& bs, double* dst
     return f(bs, dst, dst_bs, n_img, W, H, sh.rows, taps, dec, Wd, Hd, s, e0, e1);
 }
 
+template <int R, bool DECIM>
+static hipError_t launch_tile_r(const double* src, size_t src_bs, double* dst, size_t bs,
+                                int n_img, int W, int H, const BlurTaps& taps, double* dec,
+                                int Wd, int Hd, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    const dim3 grid((W + kTileW - 1) / kTileW, (H + kTileH - 1) / kTileH, n_img);
+    return launch_timed(k_blur_tile<R, DECIM>, grid, dim3(256), 0, s, e0, e1, src, src_bs, dst,
+                        bs, W, H, taps, dec, Wd, Hd);
+}
+using TileFn = hipError_t (*)(const double*, size_t, double*, size_t, int, int, int,
+                              const BlurTaps&, double*, int, int, hipStream_t, hipEvent_t,
+                              hipEvent_t);
+template <bool DECIM, int... Rs>
+struct TileTable {
+    static constexpr TileFn fns[sizeof...(Rs)] = {&launch_tile_r<Rs, DECIM>...};
+};
+template <bool DECIM, int... Rs>
+constexpr TileFn TileTable<DECIM, Rs...>::fns[sizeof...(Rs)];
+using TileDec = TileTable<true, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
+using TileNoDec = TileTable<false, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
+
 hipError_t launch_blur(const double* src, size_t src_bs, double* dst, size_t bs, int n_img, int W,
                        int H, const BlurTaps& taps, double* dec, int Wd, int Hd, double* tmp,
-                       hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+                       hipStream_t s, hipEvent_t e0, hipEvent_t e1, size_t tile_max_px) {
     const int R = taps.R;
+    if (R >= 1 && R <= kMaxTemplR && (size_t)W * H <= tile_max_px)
+        return (dec ? TileDec::fns[R - 1] : TileNoDec::fns[R - 1])(src, src_bs, dst, bs, n_img, W,
+                                                                   H, taps, dec, Wd, Hd, s, e0,
+                                                                   e1);
     if (R >= 1 && R <= kMaxTemplR) {
         const BlurSource src_desc{src, src_bs, W, H, 1};
         return launch_blur_shaped(kSrcPlane, src_desc, dst, bs, n_img, W, H, taps, dec, Wd, Hd,
@@ -1383,6 +1682,34 @@ hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int
     case NL:                                                                               \
         hipLaunchKernelGGL((k_extrema_tiles<NL>), grid, dim3(256), 0, s, d_pt, eg, thr, out, \
                            counter, cap, snap);                                            \
+        return hipGetLastError();
+        SIFT_EXT_CASE(4)
+        SIFT_EXT_CASE(5)
+        SIFT_EXT_CASE(6)
+        SIFT_EXT_CASE(7)
+        SIFT_EXT_CASE(8)
+        SIFT_EXT_CASE(9)
+        SIFT_EXT_CASE(10)
+        SIFT_EXT_CASE(11)
+        SIFT_EXT_CASE(12)
+#undef SIFT_EXT_CASE
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_extrema_stream(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
+                                 int n_gauss, int thr, sift_extremum* out, unsigned* counter,
+                                 unsigned cap, unsigned* snap, hipStream_t s) {
+    const int tasks = eg.first_tile[eg.n];
+    if (tasks == 0 || n_img == 0)
+        return snap ? launch_snapshot(counter, snap, s, 0, 3) : hipSuccess;
+    const dim3 grid((tasks + 3) / 4, n_img);
+    switch (n_gauss) {
+#define SIFT_EXT_CASE(NL)                                                                   \
+    case NL:                                                                                \
+        hipLaunchKernelGGL((k_extrema_stream<NL>), grid, dim3(256), 0, s, d_pt, eg, thr, out, \
+                           counter, cap, snap);                                             \
         return hipGetLastError();
         SIFT_EXT_CASE(4)
         SIFT_EXT_CASE(5)

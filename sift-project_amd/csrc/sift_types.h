@@ -63,13 +63,20 @@ struct PyrTable {
     int n_oct;
 };
 
+// Streaming extrema tasks: centre columns per wavefront strip (64 lanes
+// minus the two halo lanes); centre rows per task are chosen per octave.
+constexpr int kExtSpan = 62;
+
 // Flattened tile grid of one extrema launch over a set of octaves: entry i
 // (octave oct[i]) owns blocks [first_tile[i], first_tile[i+1]), tiles_x[i]
 // tiles of 64 centre columns per band of 16 centre rows; blockIdx.y = image.
+// (k_extrema_stream: "tiles" are tasks, tiles_x = strips of kExtSpan columns,
+// each task seg[i] centre rows of one strip.)
 struct ExtremaGrid {
     int n;
     int oct[kMaxOctaves];
     int tiles_x[kMaxOctaves];
+    int seg[kMaxOctaves];  // k_extrema_stream: centre rows per task
     int first_tile[kMaxOctaves + 1];
 };
 

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# torch first: it brings its own HIP runtime, and libsift_hip.so must bind to
+# the one already loaded (if the library's HIP initialises first, torch's
+# lazy init finds no device)
+import torch  # noqa: F401
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, HERE)

@@ -19,7 +19,7 @@ Each case becomes tests/golden/<name>.npz (allow_pickle=False) holding:
   pyr_sha256       sha256 of every Gaussian level, octave-major (small cases)
   input_u8         the decoded input (image1 only)
 
-usage: python tests/golden/make_goldens.py [--big] | --match
+usage: python tests/golden/make_goldens.py [--big] [names...] | --match
 """
 from __future__ import annotations
 
@@ -30,6 +30,7 @@ import struct
 import subprocess
 import sys
 import tempfile
+import zlib
 
 import numpy as np
 
@@ -37,6 +38,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "sift-project_amd"))
 from sift_hip import KP_DTYPE, synth_image  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(HERE))
+from golden_util import coords_sha256  # noqa: E402
 
 HARNESS_CF = os.path.join(ROOT, "oracle", "_ref", "ref_harness_cf")
 HARNESS_ASIS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
@@ -59,10 +63,42 @@ CASES = {
     "image1": ("image1", 0, 0, None, 0.0, 0, 3, 1, 0, "medium"),
     "synth_1920x1080": (1920, 1080, 1, None, 6.0, 42, 3, 1, 0, "medium"),
 }
+# The parameter / shape cases of tests/test_gpu_parity.py (CASES), run
+# through the reference with every detect_keypoints_and_descriptors argument
+# (sift.hh:65-71) passed explicitly: (w, h, c, seed, params). Inputs: the
+# deterministic generator, seed = crc32(name) & 0xFFFF as in that test.
+PARAM_CASES = {
+    "ragged_67x43": (67, 43, 1, {}),
+    "rgb_203x151": (203, 151, 3, {}),
+    "nodbl_rgb_250x190": (250, 190, 3, {"double_image_size": 0}),
+    "int4_180x140": (180, 140, 1, {"intervals": 4}),
+    "int1_150x110": (150, 110, 1, {"intervals": 1}),
+    "win5_170x130": (170, 130, 1, {"window_size": 5}),
+    "bins72_160x120": (160, 120, 1, {"num_bins": 72, "peak_ratio": 0.5}),
+    "lowthr_160x120": (160, 120, 1, {"contrast_threshold": 0.02, "eigen_ratio": 5.0}),
+    "oridesc_160x120": (160, 120, 1, {"ori_sigma_factor": 2.0, "desc_scale_factor": 4.0}),
+    "sigma2_140x100": (140, 100, 1, {"init_sigma": 2.0}),
+    "wide_sigma_90x70": (90, 70, 1, {"init_sigma": 6.5}),
+    "maxoct3_300x220": (300, 220, 1, {"max_octaves": 3}),
+    "tall_33x400": (33, 400, 1, {}),
+    "wide_600x20": (600, 20, 1, {}),
+}
+DEFAULT_PARAMS = {"double_image_size": 1, "init_sigma": 1.6, "intervals": 3, "window_size": 3,
+                  "contrast_threshold": 0.04, "eigen_ratio": 10.0, "num_bins": 36.0,
+                  "peak_ratio": 0.8, "ori_sigma_factor": 1.5, "desc_scale_factor": 3.0,
+                  "max_octaves": 0}
+# Real photographs (stb decode by the reference's image_io.cpp:20-35):
+# name: (path under /root/reference, crop (x0, y0, w, h) or None)
+PHOTO_CASES = {
+    "photo_cave01_00": ("stitching/collection/Dataset/CAVE-01_atrium/00.jpg", None),
+    "photo_img6121_crop960x540": ("stitching/collection/own/IMG_6121.jpg", (1536, 1242, 960, 540)),
+}
 BIG_CASES = {
     # BASELINE config 3: 4096^2, "5 octaves x 5 scales" -> intervals=2 (5 Gaussian
     # levels per octave), max_octaves=5
     "synth_4096x4096_int2_oct5": (4096, 4096, 1, 300000, 6.0, 42, 2, 1, 5, "big"),
+    # BASELINE config 5: 8K dense (1.5M blobs, sigma 1.5-5.5)
+    "synth_7680x4320_dense": (7680, 4320, 1, 1500000, 4.0, 42, 3, 1, 0, "big"),
 }
 
 
@@ -86,9 +122,14 @@ def sha(b: bytes) -> str:
     return hashlib.sha256(b).hexdigest()
 
 
-def run_harness(exe, inp, prefix, intervals, dbl, max_oct, dump):
-    subprocess.run([exe, inp, prefix, str(intervals), str(dbl), str(max_oct), str(int(dump))],
-                   check=True, stdout=subprocess.DEVNULL)
+def run_harness(exe, inp, prefix, intervals, dbl, max_oct, dump, params=None):
+    args = [exe, inp, prefix, str(intervals), str(dbl), str(max_oct), str(int(dump))]
+    if params is not None:  # the remaining sift.hh:65-71 arguments, exact reprs
+        args += [str(int(params["window_size"]))] + [
+            repr(float(params[k])) for k in ("init_sigma", "contrast_threshold", "eigen_ratio",
+                                             "num_bins", "peak_ratio", "ori_sigma_factor",
+                                             "desc_scale_factor")]
+    subprocess.run(args, check=True, stdout=subprocess.DEVNULL)
     meta = {}
     with open(prefix + ".meta.txt") as f:
         for line in f:
@@ -105,12 +146,28 @@ def load_outputs(prefix):
     return final, ext, df.reshape(-1, 128)
 
 
-def make_case(name, spec, tmp):
+def make_case(name, spec, tmp, params=None, photo=None):
     w, h, c, nb, smax, seed, intervals, dbl, max_oct, kind = spec
     inp = os.path.join(tmp, name + ".raw")
     meta = {"name": name, "intervals": intervals, "double_image_size": dbl,
             "max_octaves": max_oct, "kind": kind}
-    if w == "image1":
+    if params is not None:
+        meta["params"] = params
+    if photo is not None:
+        # stb decode by the reference harness, then (optionally) a crop
+        path, crop = photo
+        src = os.path.join("/root/reference", path)
+        probe = os.path.join(tmp, name + "_probe")
+        run_harness(HARNESS_CF, src, probe, 3, 0, 1, False)
+        decoded = read_raw(probe + ".input.raw")
+        if crop is not None:
+            x0, y0, cw, ch = crop
+            decoded = np.ascontiguousarray(decoded[y0:y0 + ch, x0:x0 + cw])
+        write_raw(inp, decoded)
+        meta["source"] = f"{path} (stb decode via reference image_io.cpp:20-35)" + (
+            f", crop x0={crop[0]} y0={crop[1]} {crop[2]}x{crop[3]}" if crop else "")
+        w = "photo"
+    elif w == "image1":
         inp = IMAGE1
         meta["source"] = "stitching/image1.jpg (stb decode via reference image_io.cpp:20-35)"
     else:
@@ -120,15 +177,22 @@ def make_case(name, spec, tmp):
                     nblobs=nb if nb is not None else max(1, (w * h) // 52), smax=smax,
                     seed=seed, input_sha256=sha(np.ascontiguousarray(img, "<f8").tobytes()))
     prefix = os.path.join(tmp, name + "_cf")
-    rm = run_harness(HARNESS_CF, inp, prefix, intervals, dbl, max_oct, kind == "small")
+    rm = run_harness(HARNESS_CF, inp, prefix, intervals, dbl, max_oct, kind == "small", params)
     final, ext, df = load_outputs(prefix)
     for k in ("octaves", "levels", "extrema", "refined", "oriented", "final"):
         meta[k] = int(rm[k][0][0])
     meta["octave_dims"] = [[int(v) for v in d[1:]] for d in rm.get("octave_dims", [])]
     meta["ref_time_s"] = {k[5:]: float(v[0][0]) for k, v in rm.items() if k.startswith("time_")}
     meta["final_sha256"] = sha(final.tobytes())
+    meta["coords_sha256"] = coords_sha256(final)
     meta["desc_f32_sha256"] = sha(df.tobytes())
     out = {}
+    if w == "photo":
+        decoded = read_raw(inp)
+        meta.update(w=decoded.shape[1], h=decoded.shape[0], c=decoded.shape[2],
+                    input_sha256=sha(np.ascontiguousarray(decoded, "<f8").tobytes()))
+        out["input_u8"] = decoded.astype(np.uint8)
+        assert np.array_equal(out["input_u8"].astype(np.float64), decoded)
     if w == "image1":
         decoded = read_raw(prefix + ".input.raw")
         meta.update(w=decoded.shape[1], h=decoded.shape[0], c=decoded.shape[2],
@@ -140,7 +204,7 @@ def make_case(name, spec, tmp):
     if kind == "small":
         # the unmodified reference must agree byte for byte
         p2 = os.path.join(tmp, name + "_asis")
-        run_harness(HARNESS_ASIS, inp, p2, intervals, dbl, max_oct, True)
+        run_harness(HARNESS_ASIS, inp, p2, intervals, dbl, max_oct, True, params)
         f2, e2, _ = load_outputs(p2)
         assert f2.tobytes() == final.tobytes(), name
         with open(prefix + ".pyr.bin", "rb") as f1, open(p2 + ".pyr.bin", "rb") as g2:
@@ -245,6 +309,20 @@ def main():
             if only and name not in only:
                 continue
             make_case(name, spec, tmp)
+        for name, (w, h, c, over) in PARAM_CASES.items():
+            gname = "case_" + name
+            if only and gname not in only:
+                continue
+            prm = dict(DEFAULT_PARAMS, **over)
+            spec = (w, h, c, None, 6.0, zlib.crc32(name.encode()) & 0xFFFF, prm["intervals"],
+                    prm["double_image_size"], prm["max_octaves"], "small")
+            make_case(gname, spec, tmp, params=prm)
+        for name, photo in PHOTO_CASES.items():
+            if only and name not in only:
+                continue
+            prm = dict(DEFAULT_PARAMS)
+            make_case(name, (0, 0, 0, None, 0.0, 0, 3, 1, 0, "medium"), tmp, params=prm,
+                      photo=photo)
 
 
 if __name__ == "__main__":

@@ -35,9 +35,21 @@ class Golden:
         return self.meta["kind"]
 
     def params(self) -> SiftParams:
-        return SiftParams(double_image_size=bool(self.meta["double_image_size"]),
-                          intervals=int(self.meta["intervals"]),
-                          max_octaves=int(self.meta["max_octaves"]))
+        """Every detect argument the reference ran with (sift.hh:65-71)."""
+        p = self.meta.get("params")
+        if p is None:  # goldens made with the defaults but these three
+            return SiftParams(double_image_size=bool(self.meta["double_image_size"]),
+                              intervals=int(self.meta["intervals"]),
+                              max_octaves=int(self.meta["max_octaves"]))
+        return SiftParams(double_image_size=bool(p["double_image_size"]),
+                          init_sigma=float(p["init_sigma"]), intervals=int(p["intervals"]),
+                          window_size=int(p["window_size"]),
+                          contrast_threshold=float(p["contrast_threshold"]),
+                          eigen_ratio=float(p["eigen_ratio"]), num_bins=float(p["num_bins"]),
+                          peak_ratio=float(p["peak_ratio"]),
+                          ori_sigma_factor=float(p["ori_sigma_factor"]),
+                          desc_scale_factor=float(p["desc_scale_factor"]),
+                          max_octaves=int(p["max_octaves"]))
 
     def input(self) -> np.ndarray:
         m = self.meta
@@ -69,3 +81,17 @@ def all_goldens(kinds=("small", "medium", "big")):
 
 def sha256_array(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+COORD_FIELDS = ("x", "y", "octave", "layer", "size")
+
+
+def coords_sha256(kps: np.ndarray) -> str:
+    """sha256 over the bit-exact fields of a final keypoint list, in order:
+    per keypoint x, y (f8), octave, layer (i4), size (f8), little-endian."""
+    dt = np.dtype([("x", "<f8"), ("y", "<f8"), ("octave", "<i4"), ("layer", "<i4"),
+                   ("size", "<f8")])
+    a = np.zeros(len(kps), dtype=dt)
+    for f in COORD_FIELDS:
+        a[f] = kps[f]
+    return hashlib.sha256(a.tobytes()).hexdigest()

@@ -71,3 +71,19 @@ def test_oracle_parameter_variants_run():
             k = run.final
             order = np.lexsort((-k["octave"], k["pori"], -k["size"], k["y"], k["x"]))
             assert np.array_equal(order, np.arange(len(k)))
+
+
+def test_parameter_cases_are_pinned_to_the_reference():
+    """Every stagewise GPU case (tests/test_gpu_parity.py CASES) has a golden
+    produced by the reference with the same input and all sift.hh:65-71
+    arguments (tests/golden/case_<name>.npz, checked above bit for bit)."""
+    import zlib
+
+    from test_gpu_parity import CASES
+
+    by_name = {g.name: g for g in GOLDENS}
+    for name, w, h, c, p in CASES:
+        g = by_name["case_" + name]
+        m = g.meta
+        assert (m["w"], m["h"], m["c"], m["seed"]) == (w, h, c, zlib.crc32(name.encode()) & 0xFFFF)
+        assert g.params() == p, name

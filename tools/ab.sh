@@ -9,8 +9,8 @@ out=gpurun_out/ab.txt
 LIBS=${LIBS:-$(ls tools/ab/*.so)}
 for rep in $(seq ${REPS:-3}); do
     for lib in $LIBS; do
-        line=$(SIFT_HIP_LIB=$(pwd)/$lib timeout -k 10 120 python bench.py --steps 40 --warmup 5 \
-            --no-cpu-baseline --no-events --no-matcher 2>/dev/null) || { echo "$lib FAILED" >> $out; exit 1; }
+        line=$(SIFT_HIP_LIB=$(pwd)/$lib timeout -k 10 120 python bench.py ${BENCH_ARGS:---steps 1000 --warmup 20} \
+            --no-cpu-baseline --no-events --no-matcher --no-extra 2>/dev/null) || { echo "$lib FAILED" >> $out; exit 1; }
         ms=$(python -c "import json,sys; print(round(json.loads(sys.argv[1])['ms_per_step'],4))" "$line")
         echo "$lib $ms" | tee -a $out
     done
