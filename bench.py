@@ -30,7 +30,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from sift_hip import INPUT_F64_DEVICE, INPUT_F64_HOST, Context, SiftParams, synth_image  # noqa: E402
+from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, PROF_EXTREMA, PROF_PYRAMID,  # noqa: E402
+                      Context, SiftParams, synth_image)
 
 METRIC = ("keypoints/sec (detect+describe) on 1920×1080; Gaussian-pyramid HBM GB/s vs peak")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -105,6 +106,39 @@ def matcher_bench(ctx, dev, kps_a, W, H, params, cpu_seconds: float) -> dict:
                                "sample": f"{nq} queries x {len(kps_b)} references, "
                                          f"oracle/sift_cpu.cpp sift_cpu_match, {t:.1f} s"}
     return out
+
+
+def load_traffic(path):
+    """PMC traffic per launch (tools/pmc_traffic.py), only if it was measured
+    on the current kernel sources."""
+    if not os.path.exists(path):
+        return None, "no PMC traffic file"
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import kernel_src_sha256
+    with open(path) as f:
+        t = json.load(f)
+    if t.get("kernel_src_sha256") != kernel_src_sha256(ROOT):
+        return None, f"stale: {os.path.relpath(path, ROOT)} was measured on other kernel sources"
+    return t, f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {os.path.relpath(path, ROOT)}"
+
+
+def roofline_obj(ms: float, nbytes: float, launches: int, traffic, note) -> dict:
+    achieved = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    alg = nbytes / launches if launches else None
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
+        "traffic_source": note,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (traffic["hbm_bytes_per_launch"] / alg)
+        if (traffic and alg) else None,
+        "avg_launch_us": (ms * 1e3 / launches) if launches else None,
+        "launches": launches,
+    }
 
 
 def pipelined(ctx, submit, n_steps: int):
@@ -193,8 +227,9 @@ def main() -> int:
     ap.add_argument("--extra-seconds", type=float, default=2.0)
     ap.add_argument("--no-events", action="store_true",
                     help="skip the per-launch HIP events of the pyramid roofline")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "blur_traffic.json"),
-                    help="PMC-derived HBM bytes per blur launch (rocprofv3 --pmc summary)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py); used only "
+                         "while its kernel-source hash matches the sources")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -270,7 +305,7 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize()
     ctx.set_profiling(not args.no_events)
-    ctx.blur_profile(reset=True)
+    ctx.profile_table(reset=True)
     t0 = time.perf_counter()
     kp_total = run(args.steps)
     if exchange is not None:
@@ -280,7 +315,11 @@ def main() -> int:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_profiling(False)
-    blur_ms, blur_launches, blur_bytes = ctx.blur_profile(reset=True)
+    prof = ctx.profile_table(reset=True)
+    pyr_rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
+    blur_ms = sum(r[0] for r in pyr_rows)
+    blur_bytes = sum(r[1] for r in pyr_rows)
+    blur_launches = sum(r[2] for r in pyr_rows)
 
     if world > 1:
         t = torch.tensor([elapsed, float(kp_total)], dtype=torch.float64, device=dev)
@@ -292,23 +331,22 @@ def main() -> int:
         kp_all = float(kp_total)
 
     if rank == 0:
-        achieved = blur_bytes / (blur_ms * 1e-3) / 1e9 if blur_ms > 0 else 0.0
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        roofline = {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "kernel": "k_blur (separable f64 Gaussian level, both passes + fused decimation)",
-            "algorithmic_bytes_per_launch": (blur_bytes / blur_launches) if blur_launches else None,
-            "avg_launch_us": (blur_ms * 1e3 / blur_launches) if blur_launches else None,
-            "launches": blur_launches,
-        }
+        traffic, traffic_note = load_traffic(args.traffic_json)
+        roofline = roofline_obj(blur_ms, blur_bytes, blur_launches,
+                                traffic.get("pyramid") if traffic else None, traffic_note)
+        roofline["kernel"] = ("Gaussian pyramid: k_blur (strip walk, octave 0 incl. the fused "
+                              "gray/x2 initial blur) + k_blur_tile (LDS tiles, octaves >= 1) + "
+                              "k_octaves_lds (LDS-resident small octaves); 16 B per pixel per "
+                              "level + 8 B per decimated pixel")
+        roofline["per_octave"] = [
+            {"octave": o, "launches": n, "us_per_launch": ms * 1e3 / n,
+             "achieved_GBps": b / (ms * 1e-3) / 1e9}
+            for o, (ms, b, n) in enumerate(pyr_rows) if n]
+        ems, eb, en = prof[PROF_EXTREMA]
+        extrema_roofline = roofline_obj(ems, eb, en, traffic.get("extrema") if traffic else None,
+                                        traffic_note)
+        extrema_roofline["kernel"] = ("k_extrema_stream (DoG on the fly, 3x3x3 non-strict test): "
+                                      "8 B x (intervals+3) levels per scanned pixel")
         out = {
             "metric": METRIC,
             "value": kp_all / elapsed,
@@ -334,6 +372,7 @@ def main() -> int:
                                                             "buffers" if world > 1 else ""),
             },
             "roofline": roofline,
+            "extrema_roofline": extrema_roofline,
         }
         out["timed_region_s"] = elapsed
         if world == 1 and not args.no_extra:

@@ -252,6 +252,16 @@ int sift_hip_set_profiling(sift_ctx* ctx, int enable);
 int sift_hip_blur_profile(sift_ctx* ctx, double* ms, int64_t* launches,
                           double* bytes, int reset);
 
+/* The same per row: SIFT_PROF_PYRAMID + o = pyramid launches of octave o
+ * (the LDS-resident small-octave launch counts under its first octave),
+ * SIFT_PROF_EXTREMA = extrema launches (algorithmic bytes: every Gaussian
+ * level read once per pixel). Each array holds SIFT_PROF_ROWS entries. */
+#define SIFT_PROF_PYRAMID 0
+#define SIFT_PROF_EXTREMA 16
+#define SIFT_PROF_ROWS 17
+int sift_hip_profile_table(sift_ctx* ctx, double* ms, double* bytes, int64_t* launches,
+                           int reset);
+
 /* ---- synthetic input (bench + tests) ----------------------------------- */
 /*
  * Deterministic synthetic gray image, bit-reproducible on any IEEE-754

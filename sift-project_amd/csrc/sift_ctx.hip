@@ -149,6 +149,7 @@ struct Stage {
 struct EventPair {
     hipEvent_t a, b;
     double bytes;
+    int row;  // profile table row (SIFT_PROF_*)
 };
 
 enum SlotState { kFree = 0, kSubmitted = 1, kFinalized = 2 };
@@ -238,11 +239,12 @@ struct sift_ctx {
     int next_ticket = 1;
     int last = -1;  // slot of the last finalised job (introspection)
 
-    // profiling (pyramid kernels)
+    // profiling: per-row kernel time / algorithmic bytes / launches
+    // (rows: pyramid launches per octave, extrema launches; SIFT_PROF_*)
     bool profiling = false;
-    double prof_ms = 0.0;
-    int64_t prof_launches = 0;
-    double prof_bytes = 0.0;
+    double prof_ms[SIFT_PROF_ROWS] = {};
+    int64_t prof_launches[SIFT_PROF_ROWS] = {};
+    double prof_bytes[SIFT_PROF_ROWS] = {};
 
     // matcher: one device arena (inputs, shifted rows, norms, results) and
     // pinned result staging
@@ -280,13 +282,13 @@ hipEvent_t sync_event(Slot& s) {  // untimed cross-stream events
 
 // Profiling events for one pyramid launch: timestamps recorded by the
 // dispatch packet itself (hipExtLaunchKernel), so timing adds no gaps.
-int prof_events(sift_ctx* ctx, Slot& s, hipEvent_t* e0, hipEvent_t* e1, double bytes) {
+int prof_events(sift_ctx* ctx, Slot& s, hipEvent_t* e0, hipEvent_t* e1, double bytes, int row) {
     *e0 = *e1 = nullptr;
     if (!ctx->profiling) return SIFT_OK;
     *e0 = pool_event(s);
     *e1 = pool_event(s);
     if (!*e0 || !*e1) return SIFT_ERR_HIP;
-    s.pending.push_back({*e0, *e1, bytes});
+    s.pending.push_back({*e0, *e1, bytes, row});
     return SIFT_OK;
 }
 
@@ -319,7 +321,8 @@ ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img, b
 
 hipError_t launch_extrema_set(const sift_ctx* ctx, const PyrTable* d_pt, const Geometry& g,
                               int o_begin, int o_end, int n_img, int thr, sift_extremum* cand,
-                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s);
+                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s,
+                              hipEvent_t e0, hipEvent_t e1);
 
 // keypoint-array capacities of a slot (per lane), all size_t and bounded so
 // that the kernels' 32-bit indices and the df32 product never wrap
@@ -458,7 +461,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         hipEvent_t e0, e1;
         const double bytes =
             n_img * (16.0 * (double)W * (double)H + (dec ? 8.0 * (double)Wd * Hd : 0.0));
-        if (prof_events(ctx, s, &e0, &e1, bytes) != SIFT_OK) return SIFT_ERR_HIP;
+        if (prof_events(ctx, s, &e0, &e1, bytes, SIFT_PROF_PYRAMID + o) != SIFT_OK)
+            return SIFT_ERR_HIP;
         double* dst = s.h_pt.lvl[o][l];
         double* decp = dec ? s.h_pt.lvl[o + 1][0] : nullptr;
         double* tmp = wide ? s.tmp.p + (o & 1) * tmp_half : nullptr;
@@ -471,7 +475,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     const int W0 = g.W[0], H0 = g.H[0];
     {
         hipEvent_t e0, e1;
-        if (prof_events(ctx, s, &e0, &e1, 16.0 * n_img * (double)W0 * H0) != SIFT_OK)
+        if (prof_events(ctx, s, &e0, &e1, 16.0 * n_img * (double)W0 * H0, SIFT_PROF_PYRAMID) !=
+            SIFT_OK)
             return SIFT_ERR_HIP;
         hipError_t err = hipSuccess;
         const bool fused = launch_blur_initial_fused(src, in_bs, s.w, s.h, s.c,
@@ -565,8 +570,14 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                             s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
                             (unsigned)s.exp_lane};
         if (tiles) {
+            // algorithmic bytes: every Gaussian level read once per pixel
+            double xb = 0.0;
+            for (int o = o_begin; o < o_end; ++o) xb += 8.0 * g.n_gauss * (double)g.W[o] * g.H[o];
+            hipEvent_t e0, e1;
+            if (prof_events(ctx, s, &e0, &e1, xb * n_img, SIFT_PROF_EXTREMA) != SIFT_OK)
+                return SIFT_ERR_HIP;
             SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
-                                            cand, live + 0, cap_cand, begin, sx));
+                                            cand, live + 0, cap_cand, begin, sx, e0, e1));
         } else {
             for (int o = o_begin; o < o_end; ++o)
                 SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], n_img, g.n_gauss,
@@ -634,7 +645,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             if (o + 1 < g.octaves) bytes += 8.0 * (double)g.W[o + 1] * (double)g.H[o + 1];
         }
         hipEvent_t e0, e1;
-        if (prof_events(ctx, s, &e0, &e1, bytes * n_img) != SIFT_OK) return SIFT_ERR_HIP;
+        if (prof_events(ctx, s, &e0, &e1, bytes * n_img, SIFT_PROF_PYRAMID + o_small) != SIFT_OK)
+            return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss, s.d_stage->taps,
                                         n_img, so, e0, e1));
     }
@@ -710,7 +722,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
             if (tiles) {
                 SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, 0, g.octaves, s.n_img,
                                                 s.dp.threshold, s.cand.p, live, cap_cand, nullptr,
-                                                sC));
+                                                sC, nullptr, nullptr));
             } else {
                 for (int o = 0; o < g.octaves; ++o)
                     SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], s.n_img, g.n_gauss,
@@ -797,9 +809,9 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
         for (const EventPair& e : s.pending) {
             float ems = 0.f;
             SIFT_HIP_TRY(hipEventElapsedTime(&ems, e.a, e.b));
-            ctx->prof_ms += ems;
-            ctx->prof_bytes += e.bytes;
-            ctx->prof_launches += 1;
+            ctx->prof_ms[e.row] += ems;
+            ctx->prof_bytes[e.row] += e.bytes;
+            ctx->prof_launches[e.row] += 1;
         }
     }
     s.pending.clear();
@@ -843,11 +855,17 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
 
 hipError_t launch_extrema_set(const sift_ctx* ctx, const PyrTable* d_pt, const Geometry& g,
                               int o_begin, int o_end, int n_img, int thr, sift_extremum* cand,
-                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s) {
+                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s,
+                              hipEvent_t e0, hipEvent_t e1) {
     const ExtremaGrid eg = extrema_grid(g, o_begin, o_end, n_img, ctx->extrema_stream);
-    return ctx->extrema_stream
-               ? launch_extrema_stream(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s)
-               : launch_extrema_tiles(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s);
+    if (ctx->extrema_stream)
+        return launch_extrema_stream(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s,
+                                     e0, e1);
+    if (e0) (void)hipEventRecord(e0, s);
+    const hipError_t e = launch_extrema_tiles(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap,
+                                              snap, s);
+    if (e1) (void)hipEventRecord(e1, s);
+    return e;
 }
 
 Slot* slot_of(sift_ctx* ctx, int ticket) {
@@ -1316,17 +1334,41 @@ int sift_hip_set_profiling(sift_ctx* ctx, int enable) {
     return SIFT_OK;
 }
 
+int sift_hip_profile_table(sift_ctx* ctx, double* ms, double* bytes, int64_t* launches,
+                           int reset) {
+    if (!ctx) return SIFT_ERR_ARG;
+    for (int r = 0; r < SIFT_PROF_ROWS; ++r) {
+        if (ms) ms[r] = ctx->prof_ms[r];
+        if (bytes) bytes[r] = ctx->prof_bytes[r];
+        if (launches) launches[r] = ctx->prof_launches[r];
+        if (reset) {
+            ctx->prof_ms[r] = 0.0;
+            ctx->prof_bytes[r] = 0.0;
+            ctx->prof_launches[r] = 0;
+        }
+    }
+    return SIFT_OK;
+}
+
 int sift_hip_blur_profile(sift_ctx* ctx, double* ms, int64_t* launches, double* bytes,
                           int reset) {
     if (!ctx) return SIFT_ERR_ARG;
-    if (ms) *ms = ctx->prof_ms;
-    if (launches) *launches = ctx->prof_launches;
-    if (bytes) *bytes = ctx->prof_bytes;
-    if (reset) {
-        ctx->prof_ms = 0.0;
-        ctx->prof_launches = 0;
-        ctx->prof_bytes = 0.0;
+    double m = 0.0, b = 0.0;
+    int64_t n = 0;
+    for (int r = SIFT_PROF_PYRAMID; r < SIFT_PROF_PYRAMID + 16; ++r) {
+        m += ctx->prof_ms[r];
+        b += ctx->prof_bytes[r];
+        n += ctx->prof_launches[r];
     }
+    if (ms) *ms = m;
+    if (launches) *launches = n;
+    if (bytes) *bytes = b;
+    if (reset)
+        for (int r = SIFT_PROF_PYRAMID; r < SIFT_PROF_PYRAMID + 16; ++r) {
+            ctx->prof_ms[r] = 0.0;
+            ctx->prof_bytes[r] = 0.0;
+            ctx->prof_launches[r] = 0;
+        }
     return SIFT_OK;
 }
 

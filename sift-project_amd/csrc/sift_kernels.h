@@ -49,7 +49,8 @@ hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int
 // streaming variant (window_size 3): eg tasks = strips x segments per octave
 hipError_t launch_extrema_stream(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
                                  int n_gauss, int thr, sift_extremum* out, unsigned* counter,
-                                 unsigned cap, unsigned* snap, hipStream_t s);
+                                 unsigned cap, unsigned* snap, hipStream_t s, hipEvent_t e0,
+                                 hipEvent_t e1);
 hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_img, int n_gauss,
                               int window_size, int thr, sift_extremum* out, unsigned* counter,
                               unsigned cap, hipStream_t s);

@@ -1700,17 +1700,20 @@ hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int
 
 hipError_t launch_extrema_stream(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
                                  int n_gauss, int thr, sift_extremum* out, unsigned* counter,
-                                 unsigned cap, unsigned* snap, hipStream_t s) {
+                                 unsigned cap, unsigned* snap, hipStream_t s, hipEvent_t e0,
+                                 hipEvent_t e1) {
     const int tasks = eg.first_tile[eg.n];
-    if (tasks == 0 || n_img == 0)
+    if (tasks == 0 || n_img == 0) {
+        if (e0) (void)hipEventRecord(e0, s);
+        if (e1) (void)hipEventRecord(e1, s);
         return snap ? launch_snapshot(counter, snap, s, 0, 3) : hipSuccess;
+    }
     const dim3 grid((tasks + 3) / 4, n_img);
     switch (n_gauss) {
 #define SIFT_EXT_CASE(NL)                                                                   \
     case NL:                                                                                \
-        hipLaunchKernelGGL((k_extrema_stream<NL>), grid, dim3(256), 0, s, d_pt, eg, thr, out, \
-                           counter, cap, snap);                                             \
-        return hipGetLastError();
+        return launch_timed(k_extrema_stream<NL>, grid, dim3(256), 0, s, e0, e1, d_pt, eg,   \
+                            thr, out, counter, cap, snap);
         SIFT_EXT_CASE(4)
         SIFT_EXT_CASE(5)
         SIFT_EXT_CASE(6)

@@ -44,6 +44,7 @@ MATCH_DTYPE = np.dtype([("i1", "<u4"), ("i2", "<u4"), ("distance", "<f8")])
 INPUT_F64_HOST, INPUT_F64_DEVICE, INPUT_U8_HOST, INPUT_U8_DEVICE = 0, 1, 2, 3
 MAX_BATCH = 16
 MAX_INFLIGHT = 2
+PROF_PYRAMID, PROF_EXTREMA, PROF_ROWS = 0, 16, 17
 
 ERRORS = {
     0: "ok",
@@ -80,6 +81,7 @@ EXPORTS = (
     "sift_hip_stream",
     "sift_hip_set_profiling",
     "sift_hip_blur_profile",
+    "sift_hip_profile_table",
     "sift_synth_image",
 )
 
@@ -187,6 +189,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sift_hip_blur_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_int64),
                                           ctypes.POINTER(ctypes.c_double), i]
+    lib.sift_hip_profile_table.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_int64), i]
     lib.sift_synth_image.argtypes = [i, i, i, ctypes.c_int64, ctypes.c_double,
                                      ctypes.c_uint64, vp]
     _lib = lib
@@ -392,6 +397,15 @@ class Context:
 
     def set_profiling(self, on: bool) -> None:
         _check(self.lib.sift_hip_set_profiling(self._ctx, 1 if on else 0))
+
+    def profile_table(self, reset: bool = False):
+        """Per-row (kernel ms, algorithmic bytes, launches): rows PROF_PYRAMID+o
+        = pyramid launches of octave o, PROF_EXTREMA = extrema launches."""
+        ms = (ctypes.c_double * PROF_ROWS)()
+        b = (ctypes.c_double * PROF_ROWS)()
+        n = (ctypes.c_int64 * PROF_ROWS)()
+        _check(self.lib.sift_hip_profile_table(self._ctx, ms, b, n, 1 if reset else 0))
+        return [(ms[r], b[r], n[r]) for r in range(PROF_ROWS)]
 
     def blur_profile(self, reset: bool = False):
         ms, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
