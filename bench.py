@@ -209,6 +209,11 @@ def extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params, seconds: float) -> d
 
 
 def main() -> int:
+    # stdout carries exactly one JSON line: keep a handle on it and send
+    # fd 1 to stderr for everything else (RCCL prints its banner to stdout)
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2500)
@@ -220,6 +225,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-matcher", action="store_true",
                     help="skip the matcher measurement (SURVEY §8f row 1)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the RCCL record exchange also at world size 1 (tests the N>1 "
+                         "data path on one GPU)")
     ap.add_argument("--sync", action="store_true",
                     help="one job at a time (no pipelining), for profiling / A-B")
     ap.add_argument("--no-extra", action="store_true",
@@ -240,7 +248,10 @@ def main() -> int:
               file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    use_exchange = world > 1 or args.exchange
+    if use_exchange:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=rank, world_size=world)
         from sift_dist import allgather_records
 
@@ -270,15 +281,19 @@ def main() -> int:
 
     def finish(ticket) -> int:
         nonlocal max_rows
+        if exchange is not None:
+            # steady state: the library writes the job's final records
+            # straight into the exchange slot in HBM (sift_hip_fetch_device),
+            # then one async RCCL all-gather per step
+            n_total = sum(ctx.wait(ticket))
+            exchange.push_device(ctx, ticket, ids)
+            return n_total
         kps, _ = ctx.fetch(ticket)
         n_total = sum(len(k) for k in kps)
-        if world > 1:
+        if use_exchange:  # warm-up: the exact two-phase exchange sizes the slots
             bufs = [torch.from_numpy(k.view(np.uint8).reshape(-1, 168)) for k in kps]
             max_rows = max(max_rows, n_total)
-            if exchange is None:
-                allgather_records([b.to(dev) for b in bufs], ids, B)
-            else:
-                exchange.push(bufs, ids)
+            allgather_records([b.to(dev) for b in bufs], ids, B)
         return n_total
 
     def run(n_steps: int) -> int:
@@ -296,9 +311,9 @@ def main() -> int:
 
     run(max(1, args.warmup))
     kp_per_image = ctx.counts()["final_n"] // B
-    if world > 1:
+    if use_exchange:
         from sift_dist import RecordExchange, agree_capacity
-        exchange = RecordExchange(agree_capacity(max_rows, dev), dev)
+        exchange = RecordExchange(agree_capacity(max_rows, dev), dev, max_images=max(16, B))
         run(1)  # one untimed pipelined step
 
     if world > 1:
@@ -321,7 +336,26 @@ def main() -> int:
     blur_bytes = sum(r[1] for r in pyr_rows)
     blur_launches = sum(r[2] for r in pyr_rows)
 
-    if world > 1:
+    exchange_check = None
+    if use_exchange:
+        # end-to-end check of the last step's exchange: every rank re-detects
+        # the next rank's images (the generator is deterministic) and compares
+        # them byte for byte with what the all-gather delivered
+        got = exchange.result((exchange.step - 1) & 1)
+        peer = (rank + 1) % world
+        ok, n_recv = 1, len(got)
+        for j in range(B):
+            i = peer * B + j
+            ref, _ = ctx.detect_device(
+                torch.from_numpy(synth_image(W, H, 1, seed=42 + i)).to(dev).data_ptr(), W, H, 1,
+                params)
+            ok &= int(i in got and got[i].cpu().numpy().tobytes() == ref.tobytes())
+        chk = torch.tensor([ok, n_recv], dtype=torch.int64, device=dev)
+        dist.all_reduce(chk[:1], op=dist.ReduceOp.MIN)
+        dist.all_reduce(chk[1:], op=dist.ReduceOp.MIN)
+        exchange_check = {"records_match_peer_redetect": bool(chk[0]),
+                          "min_images_received_per_rank": int(chk[1]),
+                          "images_per_step": world * B}
         t = torch.tensor([elapsed, float(kp_total)], dtype=torch.float64, device=dev)
         t_max = t.clone()
         dist.all_reduce(t_max[:1], op=dist.ReduceOp.MAX)
@@ -368,13 +402,16 @@ def main() -> int:
                 "image": f"{W}x{H}x1",
                 "images_per_gpu_per_step": B,
                 "keypoints_per_image": kp_per_image,
-                "parallelism": f"image-sharded x{world}" + (", RCCL all-gather of descriptor "
-                                                            "buffers" if world > 1 else ""),
+                "parallelism": f"image-sharded x{world}" + (
+                    ", RCCL all-gather of the descriptor records straight from HBM "
+                    "(sift_hip_fetch_device), pipelined one step behind" if world > 1 else ""),
             },
             "roofline": roofline,
             "extrema_roofline": extrema_roofline,
         }
         out["timed_region_s"] = elapsed
+        if exchange_check is not None:
+            out["exchange_check"] = exchange_check
         if world == 1 and not args.no_extra:
             out.update(extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params,
                                   args.extra_seconds))
@@ -384,10 +421,10 @@ def main() -> int:
             kps_a, _ = ctx.detect_device(dev_imgs[0].data_ptr(), W, H, 1, params)
             out["matcher"] = matcher_bench(ctx, dev, kps_a, W, H, params,
                                            0.0 if args.no_cpu_baseline else args.cpu_seconds)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
 
     ctx.close()
-    if world > 1:
+    if use_exchange:
         dist.destroy_process_group()
     return 0
 

@@ -166,6 +166,14 @@ int sift_hip_wait(sift_ctx* ctx, int ticket, size_t* counts, size_t* total);
  * releases it without copying. Waits first if needed. */
 int sift_hip_fetch(sift_ctx* ctx, int ticket, sift_kp* out, float* desc_f32);
 
+/* Same as sift_hip_fetch, but the records go to DEVICE memory d_out (cap
+ * records, on the context's device; image-major, identical bytes): gathered
+ * on the device from the records the kernels left in HBM, only a 12-byte
+ * (index, size) pair per keypoint crosses PCIe. Complete on return. Used by
+ * the multi-GPU driver to feed the RCCL all-gather straight from HBM.
+ * SIFT_ERR_ARG (job kept) when cap < the job's total. */
+int sift_hip_fetch_device(sift_ctx* ctx, int ticket, void* d_out, size_t cap);
+
 /* submit + wait + fetch into library-allocated storage (sift_hip_free):
  * *out_kps image-major, counts[b] per image. */
 int sift_hip_detect_batch(sift_ctx* ctx, const void* const* images, int n_images,

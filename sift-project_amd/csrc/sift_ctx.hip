@@ -213,6 +213,8 @@ struct Slot {
     Pinned<sift_kp> h_ori;
     Pinned<RecSide> h_side;
     Pinned<float> h_df32;
+    Pinned<GatherItem> h_gather;  // fetch_device: (record index, size) per final record
+    DevBuf<GatherItem> d_gather;
     sift_counts counts{};
     clk::time_point t_submit;
     double t_host[5] = {0, 0, 0, 0, 0};
@@ -508,7 +510,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // launch (k_octaves_lds); the larger ones get one k_blur launch per level
     int o_small = g.octaves;
     for (int o = 0; o < g.octaves; ++o)
-        if ((size_t)g.W[o] * g.H[o] <= (size_t)kLdsOctavePx) {
+        if (lds_octave_fits(g.W[o], g.H[o])) {
             o_small = o;
             break;
         }
@@ -954,6 +956,34 @@ void gather(Slot& s, sift_kp* out, float* df) {
     s.t_host[4] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
 }
 
+// final records of a finalised job into device memory, ordered on the
+// slot's keypoint stream and completed before return
+int gather_device(Slot& s, sift_kp* d_out) {
+    const size_t n = s.n_final;
+    if (n == 0) return SIFT_OK;
+    int st;
+    if ((st = s.h_gather.ensure(n)) != SIFT_OK || (st = s.d_gather.ensure(n)) != SIFT_OK)
+        return st;
+    for (size_t i = 0; i < n; ++i) {
+        const unsigned pos = s.keep[i];  // host position of the record
+        int L;
+        size_t j;
+        if (s.exported) {
+            L = (int)(pos / s.exp_lane);
+            j = pos - (size_t)L * s.exp_lane;
+        } else {
+            L = pos < s.n_lane[0] ? 0 : 1;
+            j = pos - (L ? s.n_lane[0] : 0);
+        }
+        s.h_gather.p[i] = GatherItem{s.rec_src[pos].size, (unsigned)(L * s.cap_ori + j), 0};
+    }
+    SIFT_HIP_TRY(hipMemcpyAsync(s.d_gather.p, s.h_gather.p, n * sizeof(GatherItem),
+                                hipMemcpyHostToDevice, s.sC));
+    SIFT_HIP_TRY(launch_gather_records(s.ori.p, s.d_gather.p, (unsigned)n, d_out, s.sC));
+    SIFT_HIP_TRY(hipStreamSynchronize(s.sC));
+    return SIFT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1050,6 +1080,8 @@ int sift_hip_destroy(sift_ctx* ctx) {
         s.h_ori.release();
         s.h_side.release();
         s.h_df32.release();
+        s.h_gather.release();
+        s.d_gather.release();
         for (hipEvent_t e : s.chain_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : s.sync_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : s.ev_pool) (void)hipEventDestroy(e);
@@ -1093,6 +1125,20 @@ int sift_hip_fetch(sift_ctx* ctx, int ticket, sift_kp* out, float* desc_f32) {
     s->state = kFree;
     s->ticket = -1;
     return SIFT_OK;
+}
+
+int sift_hip_fetch_device(sift_ctx* ctx, int ticket, void* d_out, size_t cap) {
+    if (!ctx || (!d_out && cap)) return SIFT_ERR_ARG;
+    Slot* s = slot_of(ctx, ticket);
+    if (!s) return SIFT_ERR_STATE;
+    int st = wait_impl(ctx, *s);
+    if (st != SIFT_OK) return st;
+    if (cap < s->n_final) return SIFT_ERR_ARG;  // the job stays fetchable
+    (void)hipSetDevice(ctx->device);
+    st = gather_device(*s, static_cast<sift_kp*>(d_out));
+    s->state = kFree;
+    s->ticket = -1;
+    return st;
 }
 
 int sift_hip_detect_batch(sift_ctx* ctx, const void* const* images, int n_images,

@@ -76,6 +76,10 @@ hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* 
                              unsigned* work, const ExportSink& ex, unsigned wgs,
                              hipStream_t s);
 
+// out[i] = recs[items[i].src] with size = items[i].size (final records on the device)
+hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, unsigned n,
+                                 sift_kp* out, hipStream_t s);
+
 // Matcher (sift_match.hip): records -> shifted descriptor rows + norms
 // (n_pad a multiple of 32, rows [n, n_pad) padding), then the 2-NN ratio test
 // of queries [0, n1) against the n2_pad reference rows: out_j[i] = index of

@@ -401,12 +401,12 @@ static_assert(kTileH == 4 * 8, "column pass: 256 threads = 64 columns x 4 runs o
 // time; the radius is a template parameter so the taps sit in registers.
 // ---------------------------------------------------------------------------
 struct LdsLevel {
-    double* A;  // current level (in: previous level, out: this level)
-    double* T;  // horizontal-pass temporary
-    double* D;  // next octave base (when dec)
-    double* g;  // global plane of this level
-    double* gd; // global plane of the next octave's base (when dec)
-    int W, H, Wd, Hd;
+    double* A;  // current level (in: previous level, out: this level), row stride P
+    double* T;  // horizontal-pass temporary, row stride P
+    double* D;  // next octave base (when dec), row stride Pd
+    double* g;  // global plane of this level (row stride W)
+    double* gd; // global plane of the next octave's base (when dec, row stride Wd)
+    int W, H, Wd, Hd, P, Pd;
     bool dec;
 };
 
@@ -414,7 +414,9 @@ struct LdsLevel {
 // x in the row pass, along y in the column pass), loads the run plus its 2R
 // halo once from LDS and evaluates the kLdsRun independent dependency chains
 // interleaved (one output per thread was LDS- and latency-bound: 2R+1 reads
-// and one serial chain per output, on one CU).
+// and one serial chain per output, on one CU). Row-pass tasks go lane-per-
+// row and the odd stride P keeps those lanes on different banks (a lane-per-
+// run mapping measured 6.7 bank-conflict cycles per LDS instruction).
 constexpr int kLdsRun = 8;
 
 template <int R>
@@ -424,13 +426,13 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
 #pragma unroll
     for (int u = 0; u <= R; ++u) k[u] = t.k[u];
     const double sw = t.sum_w, inv = t.inv;
-    const int W = L.W, H = L.H;
+    const int W = L.W, H = L.H, P = L.P;
     // row pass (image.cpp:170-185): task = (row y, run of columns from x0)
     const int rx = (W + kLdsRun - 1) / kLdsRun;
     for (int task = threadIdx.x; task < H * rx; task += blockDim.x) {
-        const int y = task / rx;
-        const int x0 = (task - y * rx) * kLdsRun;
-        const double* row = L.A + y * W;
+        const int x0 = (task / H) * kLdsRun;
+        const int y = task - (x0 / kLdsRun) * H;
+        const double* row = L.A + y * P;
         double v[NV];
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] = row[clampi(x0 - R + i, 0, W - 1)];
@@ -443,7 +445,7 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
             for (int j = 0; j < kLdsRun; ++j) acc[j] += k[u] * (v[j + R + u] + v[j + R - u]);
 #pragma unroll
         for (int j = 0; j < kLdsRun; ++j)
-            if (x0 + j < W) L.T[y * W + x0 + j] = div_sum_w(acc[j], sw, inv);
+            if (x0 + j < W) L.T[y * P + x0 + j] = div_sum_w(acc[j], sw, inv);
     }
     __syncthreads();
     // column pass (image.cpp:193-208): task = (column x, run of rows from y0);
@@ -455,7 +457,7 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
         const int y0 = yr * kLdsRun;
         double v[NV];
 #pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = L.T[clampi(y0 - R + i, 0, H - 1) * W + x];
+        for (int i = 0; i < NV; ++i) v[i] = L.T[clampi(y0 - R + i, 0, H - 1) * P + x];
         double acc[kLdsRun];
 #pragma unroll
         for (int j = 0; j < kLdsRun; ++j) acc[j] = v[j + R] * k[0];
@@ -468,10 +470,10 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
             const int y = y0 + j;
             if (y < H) {
                 const double o = div_sum_w(acc[j], sw, inv);
-                L.A[y * W + x] = o;
+                L.A[y * P + x] = o;
                 L.g[y * W + x] = o;
                 if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
-                    L.D[(y >> 1) * L.Wd + (x >> 1)] = o;
+                    L.D[(y >> 1) * L.Pd + (x >> 1)] = o;
                     L.gd[(y >> 1) * L.Wd + (x >> 1)] = o;
                 }
             }
@@ -482,26 +484,26 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
 
 __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int W = L.W, H = L.H, R = t.R;
+    const int W = L.W, H = L.H, R = t.R, P = L.P;
     for (int y = ty; y < H; y += 16) {
-        const double* row = L.A + y * W;
+        const double* row = L.A + y * P;
         for (int x = tx; x < W; x += 64) {
             double acc = row[x] * t.k[0];
             for (int u = 1; u <= R; ++u) acc += t.k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
-            L.T[y * W + x] = acc / t.sum_w;
+            L.T[y * P + x] = acc / t.sum_w;
         }
     }
     __syncthreads();
     for (int y = ty; y < H; y += 16) {
         for (int x = tx; x < W; x += 64) {
-            double acc = L.T[y * W + x] * t.k[0];
+            double acc = L.T[y * P + x] * t.k[0];
             for (int u = 1; u <= R; ++u)
-                acc += t.k[u] * (L.T[min(y + u, H - 1) * W + x] + L.T[max(y - u, 0) * W + x]);
+                acc += t.k[u] * (L.T[min(y + u, H - 1) * P + x] + L.T[max(y - u, 0) * P + x]);
             const double v = acc / t.sum_w;
-            L.A[y * W + x] = v;
+            L.A[y * P + x] = v;
             L.g[y * W + x] = v;
             if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
-                L.D[(y >> 1) * L.Wd + (x >> 1)] = v;
+                L.D[(y >> 1) * L.Pd + (x >> 1)] = v;
                 L.gd[(y >> 1) * L.Wd + (x >> 1)] = v;
             }
         }
@@ -520,9 +522,12 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
     double* T = lds + kLdsOctavePx;          // horizontal-pass temporary
     double* D = lds + 2 * kLdsOctavePx;      // next octave's base
     {
-        const int W = pt->w[o_first], H = pt->h[o_first];
+        const int W = pt->w[o_first], H = pt->h[o_first], P = W | 1;
         const double* g0 = plane(pt, b, o_first, 0);
-        for (int i = tid; i < W * H; i += nt) A[i] = g0[i];
+        for (int i = tid; i < W * H; i += nt) {
+            const int y = i / W;
+            A[y * P + (i - y * W)] = g0[i];
+        }
     }
     __syncthreads();
     for (int o = o_first; o <= o_last; ++o) {
@@ -533,8 +538,10 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
         L.D = D;
         L.W = pt->w[o];
         L.H = pt->h[o];
+        L.P = L.W | 1;
         L.Wd = has_next ? pt->w[o + 1] : 0;
         L.Hd = has_next ? pt->h[o + 1] : 0;
+        L.Pd = L.Wd | 1;
         L.gd = has_next ? const_cast<double*>(plane(pt, b, o + 1, 0)) : nullptr;
         for (int l = 1; l < n_gauss; ++l) {
             L.g = const_cast<double*>(plane(pt, b, o, l));
@@ -554,8 +561,8 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
                     lds_level_any(L, t);
             }
         }
-        if (has_next) {
-            for (int i = tid; i < L.Wd * L.Hd; i += nt) A[i] = D[i];
+        if (has_next) {  // next base becomes the current level (same stride Pd)
+            for (int i = tid; i < L.Pd * L.Hd; i += nt) A[i] = D[i];
             __syncthreads();
         }
     }
@@ -1657,6 +1664,28 @@ hipError_t launch_u8_to_f64(const uint8_t* in, double* out, size_t n, hipStream_
     const size_t threads = (n + 7) / 8;
     hipLaunchKernelGGL(k_u8_to_f64, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, in,
                        out, n);
+    return hipGetLastError();
+}
+
+// Final records of a job gathered on the device: out[i] = recs[src[i]]
+// with the host's glibc-exact size (sift.cpp:427-429) patched in. One
+// 64-lane wave per record, 168 B = 21 doubles.
+__global__ __launch_bounds__(256) void k_gather_records(const sift_kp* __restrict__ recs,
+                                                        const GatherItem* __restrict__ items,
+                                                        unsigned n, sift_kp* __restrict__ out) {
+    const unsigned i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= n) return;
+    const GatherItem it = items[i];
+    const double* src = reinterpret_cast<const double*>(recs + it.src);
+    double* dst = reinterpret_cast<double*>(out + i);
+    if (lane < 21) dst[lane] = (lane == 3) ? it.size : src[lane];  // size @ byte 24
+}
+
+hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, unsigned n,
+                                 sift_kp* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_records, dim3((n + 3) / 4), dim3(256), 0, s, recs, items, n, out);
     return hipGetLastError();
 }
 

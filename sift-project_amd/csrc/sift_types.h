@@ -32,6 +32,13 @@ constexpr int kMaxBins = 256;     // orientation bins supported
 // quarter-size next base = 2.25 * 9088 * 8 B = 163,584 B of the 163,840 B LDS
 constexpr int kLdsOctavePx = 9088;
 constexpr size_t kLdsOctaveBytes = (2 * (size_t)kLdsOctavePx + kLdsOctavePx / 4) * sizeof(double);
+// planes live in LDS with an odd row stride (W | 1 doubles: lane-per-row
+// accesses spread over the banks); an octave fits when its level and the
+// next octave's base do
+inline constexpr bool lds_octave_fits(int W, int H) {
+    return (size_t)(W | 1) * H <= (size_t)kLdsOctavePx &&
+           (size_t)((W / 2) | 1) * (H / 2) <= (size_t)kLdsOctavePx / 4;
+}
 
 // Half kernel of apply_gaussian_blur_fast (image.cpp:226-235) plus its
 // normalising sum (image.cpp:171-185), computed on the host with glibc.
@@ -113,6 +120,14 @@ struct RawKp {
 struct RecSide {
     double off0;
     int img, pad;
+};
+
+// One final record for the device-side gather (sift_hip_fetch_device):
+// its index in the job's device record array and its glibc-exact size.
+struct GatherItem {
+    double size;
+    unsigned src;
+    unsigned pad;
 };
 
 // Where k_descriptor also writes each finished record (mapped, coherent

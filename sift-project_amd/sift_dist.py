@@ -1,5 +1,5 @@
-"""Multi-GPU batch driver pieces: one image per GPU, RCCL all-gather of the
-per-image descriptor buffers.
+"""Multi-GPU batch driver pieces: images sharded over GPUs, RCCL all-gather of
+the per-image descriptor buffers.
 
 detect_keypoints_and_descriptors is a pure function of one image
 (reference src/sift.cpp:712-776), so a batch shards by image with no
@@ -14,6 +14,7 @@ with device tensors, "gloo" with CPU tensors (the CPU tests).
 """
 from __future__ import annotations
 
+import math
 from typing import Dict, List, Sequence
 
 import torch
@@ -22,23 +23,32 @@ import torch.distributed as dist
 RECORD_BYTES = 168
 
 
+def collective_device(group=None) -> torch.device:
+    """The device this group's collectives run on: the current CUDA (HIP)
+    device under nccl (RCCL), the CPU under gloo."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def shard(n_images: int, rank: int, world: int) -> List[int]:
     """Image indices owned by `rank` (round-robin, config 4: i -> GPU i % 8)."""
     return list(range(rank, n_images, world))
 
 
 def allgather_records(local: Sequence[torch.Tensor], image_ids: Sequence[int],
-                      max_local: int, group=None) -> Dict[int, torch.Tensor]:
-    """All-gather per-image record buffers.
+                      max_local: int, group=None, device=None) -> Dict[int, torch.Tensor]:
+    """All-gather per-image record buffers (exact two-phase exchange).
 
-    local      uint8 tensors of shape [n_i, 168], one per local image, all on
-               the same device (the collective's device)
+    local      uint8 tensors of shape [n_i, 168], one per local image
     image_ids  global image index of each local buffer
     max_local  max images per rank (same on every rank)
+    device     the collective's device (default: collective_device(group));
+               every rank uses it, also a rank without images
     Returns {image_id: uint8 [n, 168]} for every image of every rank.
     """
     world = dist.get_world_size(group)
-    dev = local[0].device if len(local) else torch.device("cpu")
+    dev = device if device is not None else collective_device(group)
     if len(local) != len(image_ids) or len(local) > max_local:
         raise ValueError("inconsistent local buffers")
     meta = torch.full((max_local, 2), -1, dtype=torch.int64, device=dev)
@@ -53,7 +63,7 @@ def allgather_records(local: Sequence[torch.Tensor], image_ids: Sequence[int],
     max_rows = max(max(rows), 1)
     payload = torch.zeros((max_rows, RECORD_BYTES), dtype=torch.uint8, device=dev)
     if len(local):
-        cat = torch.cat(list(local), dim=0)
+        cat = torch.cat([t.to(dev) for t in local], dim=0)
         payload[: cat.shape[0]] = cat
     gathered = [torch.empty_like(payload) for _ in range(world)]
     dist.all_gather(gathered, payload, group=group)
@@ -74,27 +84,34 @@ class RecordExchange:
 
     One collective per step, no count exchange and no host synchronisation:
     every rank sends a fixed-capacity slot (`cap_rows` records of 168 B after
-    a 168-byte header row holding the image count and per-image
-    (image id, record count) pairs), with ``all_gather_into_tensor``
-    issued asynchronously on a side stream, so step i's exchange overlaps
-    step i+1's detection. Slots are double-buffered; a slot is refilled only
-    after the collective that last read it has completed. `cap_rows` must be
-    the same on every rank (see ``agree_capacity``). Every rank always takes
-    part in the same collective (no per-rank fallback that could diverge): a
-    slot that overflows is sent truncated with its true count, and
-    ``result`` raises for it; ``allgather_records`` is the exact two-phase
-    exchange for callers that cannot bound the counts.
+    header rows holding the image count, the record count and per-image
+    (image id, record count) pairs for up to `max_images` images), with
+    ``all_gather_into_tensor`` issued asynchronously on a side stream, so
+    step i's exchange overlaps step i+1's detection. Slots are
+    double-buffered; a slot is refilled only after the collective that last
+    read it has completed. `cap_rows` must be the same on every rank (see
+    ``agree_capacity``). Every rank always takes part in the same collective
+    (no per-rank fallback that could diverge): a slot that overflows is sent
+    truncated with its true count, and ``result`` raises for it;
+    ``allgather_records`` is the exact two-phase exchange for callers that
+    cannot bound the counts.
+
+    ``push`` takes host buffers (staged through pinned memory); ``push_device``
+    takes a submitted detect job and has the library write its final records
+    straight into the device slot (sift_hip_fetch_device: gathered on the GPU
+    from the records in HBM), so the payload never crosses PCIe.
     """
 
-    MAX_IMAGES = 9  # (id, count) pairs in the 168-byte header row (int64 x 20)
-
-    def __init__(self, cap_rows: int, device: torch.device, group=None):
+    def __init__(self, cap_rows: int, device: torch.device, group=None, max_images: int = 16):
         self.group = group
         self.world = dist.get_world_size(group)
         self.cap = int(cap_rows)
         self.device = device
         self.cuda = device.type == "cuda"
-        rows = self.cap + 1
+        self.max_images = int(max_images)
+        self.hdr_words = 2 + 2 * self.max_images
+        self.hdr_rows = math.ceil(self.hdr_words * 8 / RECORD_BYTES)
+        rows = self.cap + self.hdr_rows
         pin = self.cuda
         self.host = [torch.zeros((rows, RECORD_BYTES), dtype=torch.uint8, pin_memory=pin)
                      for _ in range(2)]
@@ -113,32 +130,31 @@ class RecordExchange:
             self.done[s] = None
             self.work[s] = None
 
-    def push(self, local: Sequence[torch.Tensor], image_ids: Sequence[int]) -> int:
-        """Start the exchange of this step's buffers (uint8 [n_i, 168], host);
-        returns the slot index whose `gathered` buffer will hold the result."""
-        if len(local) > self.MAX_IMAGES:
-            raise ValueError("too many images per step for the header row")
-        n_rows = sum(int(t.shape[0]) for t in local)
+    def _next_slot(self) -> int:
         s = self.step & 1
         self.step += 1
         self._wait_slot(s)
-        h = self.host[s]
-        hdr = torch.zeros(2 + 2 * self.MAX_IMAGES, dtype=torch.int64)
-        hdr[0] = len(local)
-        hdr[1] = n_rows
-        for j, (t, i) in enumerate(zip(local, image_ids)):
+        return s
+
+    def _header(self, counts: Sequence[int], image_ids: Sequence[int]) -> torch.Tensor:
+        if len(counts) > self.max_images:
+            raise ValueError(f"{len(counts)} images per step > max_images={self.max_images}")
+        hdr = torch.zeros(self.hdr_rows * RECORD_BYTES // 8, dtype=torch.int64)
+        hdr[0] = len(counts)
+        hdr[1] = sum(int(c) for c in counts)
+        for j, (c, i) in enumerate(zip(counts, image_ids)):
             hdr[2 + 2 * j] = int(i)
-            hdr[3 + 2 * j] = int(t.shape[0])
-        h[0, : hdr.numel() * 8] = hdr.view(torch.uint8)
-        off = 1
-        for t in local:  # a slot that overflows is truncated and flagged
-            n = min(int(t.shape[0]), self.cap + 1 - off)
-            h[off: off + n] = t[:n]
-            off += n
+            hdr[3 + 2 * j] = int(c)
+        return hdr.view(torch.uint8)
+
+    def _launch(self, s: int, n_host_bytes: int) -> None:
+        """Copy the slot's first n_host_bytes from its pinned staging and
+        start the all-gather (async on the side stream for cuda)."""
         if self.cuda:
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.stream):
-                self.dev[s][: off].copy_(h[: off], non_blocking=True)
+                self.dev[s].view(-1)[:n_host_bytes].copy_(self.host[s].view(-1)[:n_host_bytes],
+                                                          non_blocking=True)
                 self.work[s] = dist.all_gather_into_tensor(self.gathered[s], self.dev[s],
                                                            group=self.group, async_op=True)
                 self.work[s].wait()  # orders the side stream after the collective
@@ -146,10 +162,43 @@ class RecordExchange:
                 ev.record(self.stream)
                 self.done[s] = ev
         else:
-            self.dev[s][: off] = h[: off]
+            self.dev[s].view(-1)[:n_host_bytes] = self.host[s].view(-1)[:n_host_bytes]
             self.work[s] = dist.all_gather_into_tensor(self.gathered[s], self.dev[s],
                                                        group=self.group, async_op=True)
             self.done[s] = self.work[s]
+
+    def push(self, local: Sequence[torch.Tensor], image_ids: Sequence[int]) -> int:
+        """Start the exchange of this step's buffers (uint8 [n_i, 168], host);
+        returns the slot index whose `gathered` buffer will hold the result."""
+        s = self._next_slot()
+        h = self.host[s]
+        hdr = self._header([int(t.shape[0]) for t in local], image_ids)
+        h.view(-1)[: hdr.numel()] = hdr
+        off = self.hdr_rows
+        for t in local:  # a slot that overflows is truncated and flagged
+            n = min(int(t.shape[0]), self.cap + self.hdr_rows - off)
+            h[off: off + n] = t[:n]
+            off += n
+        self._launch(s, off * RECORD_BYTES)
+        return s
+
+    def push_device(self, sift_ctx, ticket: int, image_ids: Sequence[int]) -> int:
+        """Start the exchange of a submitted detect job's records: the
+        library writes them into the device slot (no host copy of the
+        payload; only the header goes through pinned staging)."""
+        counts = sift_ctx.wait(ticket)
+        n_rows = sum(counts)
+        s = self._next_slot()
+        base = self.dev[s][self.hdr_rows:]
+        if n_rows <= self.cap:
+            sift_ctx.fetch_device(ticket, base.data_ptr(), self.cap)
+        else:  # overflow: truncated and flagged, as push does
+            tmp = torch.empty((n_rows, RECORD_BYTES), dtype=torch.uint8, device=self.device)
+            sift_ctx.fetch_device(ticket, tmp.data_ptr(), n_rows)
+            base.copy_(tmp[: self.cap])
+        hdr = self._header(counts, image_ids)
+        self.host[s].view(-1)[: hdr.numel()] = hdr
+        self._launch(s, hdr.numel())
         return s
 
     def flush(self) -> None:
@@ -159,15 +208,15 @@ class RecordExchange:
 
     def result(self, s: int) -> Dict[int, torch.Tensor]:
         """{image_id: uint8 [n, 168]} of a completed slot (call flush first)."""
-        rows = self.cap + 1
+        rows = self.cap + self.hdr_rows
         out: Dict[int, torch.Tensor] = {}
         g = self.gathered[s].view(self.world, rows, RECORD_BYTES)
         for r in range(self.world):
-            hdr = g[r, 0, : (2 + 2 * self.MAX_IMAGES) * 8].cpu().view(torch.int64)
+            hdr = g[r, : self.hdr_rows].reshape(-1)[: self.hdr_words * 8].cpu().view(torch.int64)
             if int(hdr[1]) > self.cap:
                 raise RuntimeError(f"rank {r} sent {int(hdr[1])} records into a slot of "
                                    f"{self.cap}: raise the capacity (agree_capacity slack)")
-            off = 1
+            off = self.hdr_rows
             for j in range(int(hdr[0])):
                 n = int(hdr[3 + 2 * j])
                 out[int(hdr[2 + 2 * j])] = g[r, off: off + n]

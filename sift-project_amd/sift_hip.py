@@ -70,6 +70,7 @@ EXPORTS = (
     "sift_hip_submit",
     "sift_hip_wait",
     "sift_hip_fetch",
+    "sift_hip_fetch_device",
     "sift_hip_detect_batch",
     "sift_hip_match",
     "sift_hip_match_device",
@@ -172,6 +173,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                     ctypes.POINTER(CParams), i, ctypes.POINTER(i)]
     lib.sift_hip_wait.argtypes = [vp, i, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     lib.sift_hip_fetch.argtypes = [vp, i, vp, vp]
+    lib.sift_hip_fetch_device.argtypes = [vp, i, vp, sz]
     lib.sift_hip_detect_batch.argtypes = [vp, ctypes.POINTER(vp), i, i, i, i, i,
                                           ctypes.POINTER(CParams), ctypes.POINTER(vp),
                                           ctypes.POINTER(sz), ctypes.POINTER(vp)]
@@ -289,6 +291,14 @@ class Context:
         k = [kps[offs[b]:offs[b + 1]] for b in range(n)]
         d = [df[offs[b]:offs[b + 1]] for b in range(n)] if want_f32 else None
         return k, d
+
+    def fetch_device(self, ticket: int, dev_ptr: int, cap: int):
+        """Final records of a job written to device memory (image-major, cap
+        records available); per-image counts. Releases the job."""
+        counts = self.wait(ticket)
+        _check(self.lib.sift_hip_fetch_device(self._ctx, ticket, ctypes.c_void_p(dev_ptr), cap))
+        del self._jobs[ticket]
+        return counts
 
     def detect(self, img: np.ndarray, params: SiftParams | None = None, desc_f32: bool = False):
         """detect_keypoints_and_descriptors on a host image (H,W[,C] float64)."""

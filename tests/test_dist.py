@@ -40,7 +40,7 @@ def _worker(rank, world, port, n_images, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_images", [(2, 5), (3, 7), (2, 2)])
+@pytest.mark.parametrize("world,n_images", [(2, 5), (3, 7), (2, 2), (3, 2)])
 def test_allgather_records_gloo(world, n_images):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -122,3 +122,38 @@ def test_record_exchange_gloo():
         for r in range(world):
             assert res[r][1][step] == want
     assert res[0][1][2] is None and res[1][1][2] is None
+
+
+def _many_images_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids = shard(12 * world, rank, world)  # 12 images per rank and step
+        ex = RecordExchange(4096, torch.device("cpu"), max_images=16)
+        bufs = [torch.from_numpy(_records(7, i, 3 + i % 5)) for i in ids]
+        s = ex.push(bufs, ids)
+        ex.flush()
+        out_q.put((rank, {k: v.numpy().tobytes() for k, v in ex.result(s).items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_record_exchange_many_images_gloo():
+    """More images per step than one 168-byte header row holds (the round-1
+    exchange capped a step at 9 images)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_many_images_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {i: _records(7, i, 3 + i % 5).tobytes() for i in range(12 * world)}
+    for r in range(world):
+        assert res[r] == want

@@ -181,5 +181,22 @@ def test_gpu_batch_record_exchange_world1(gpu_ctx):
         res = ex.result(s)
         for i in ids:
             assert res[i].cpu().numpy().tobytes() == kps[i].tobytes()
+        # device path: the library writes the job's final records straight
+        # into the exchange slot (sift_hip_fetch_device), same bytes
+        from sift_hip import INPUT_F64_HOST
+        for step in range(3):  # both slots, then reuse
+            t = gpu_ctx.submit(imgs, INPUT_F64_HOST, 480, 360, 1)
+            s = ex.push_device(gpu_ctx, t, ids)
+            ex.flush()
+            res = ex.result(s)
+            for i in ids:
+                assert res[i].cpu().numpy().tobytes() == kps[i].tobytes(), (step, i)
+        # too small a destination keeps the job; then it can still be fetched
+        t = gpu_ctx.submit(imgs[:1], INPUT_F64_HOST, 480, 360, 1)
+        small = torch.empty((1, RECORD_BYTES), dtype=torch.uint8, device=dev)
+        with pytest.raises(RuntimeError, match="invalid argument"):
+            gpu_ctx.fetch_device(t, small.data_ptr(), 1)
+        k, _ = gpu_ctx.fetch(t)
+        assert k[0].tobytes() == kps[0].tobytes()
     finally:
         dist.destroy_process_group()
