@@ -19,7 +19,7 @@ Each case becomes tests/golden/<name>.npz (allow_pickle=False) holding:
   pyr_sha256       sha256 of every Gaussian level, octave-major (small cases)
   input_u8         the decoded input (image1 only)
 
-usage: python tests/golden/make_goldens.py [--big] [names...] | --match
+usage: python tests/golden/make_goldens.py [--big] [names...] | --match | --cli
 """
 from __future__ import annotations
 
@@ -292,6 +292,30 @@ def make_match(tmp):
     np.savez_compressed(os.path.join(HERE, "match_cases.npz"), **out)
 
 
+def make_cli(tmp):
+    """tests/golden/cli_outputs.json + the two input images: the reference
+    CLI (main.cpp:6-19, copy-fixed build oracle/_ref/sift_cf) on
+    stitching/image1.jpg and image2.jpg; sha256 of the keypoints.png (written
+    by every detect, sift.cpp:765-768: the last one, image2's) and
+    matches.png (sift.cpp:850-876) it leaves behind."""
+    import shutil
+    cli = os.path.join(ROOT, "oracle", "_ref", "sift_cf")
+    for src, dst in ((IMAGE1, "cli_image1.jpg"), (IMAGE2, "cli_image2.jpg")):
+        shutil.copyfile(src, os.path.join(HERE, dst))
+        shutil.copyfile(src, os.path.join(tmp, dst))
+    subprocess.run([cli, "cli_image1.jpg", "cli_image2.jpg"], cwd=tmp, check=True,
+                   stdout=subprocess.DEVNULL)
+    res = {"command": "sift cli_image1.jpg cli_image2.jpg (reference main.cpp, copy-fixed "
+                      "sift.cpp, oracle/_ref/sift_cf)",
+           "inputs": {n: sha(open(os.path.join(HERE, n), "rb").read())
+                      for n in ("cli_image1.jpg", "cli_image2.jpg")}}
+    for f in ("keypoints.png", "matches.png"):
+        res[f] = sha(open(os.path.join(tmp, f), "rb").read())
+    with open(os.path.join(HERE, "cli_outputs.json"), "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print("cli:", res)
+
+
 def main():
     for exe in (HARNESS_CF, HARNESS_ASIS):
         if not os.path.exists(exe):
@@ -300,6 +324,10 @@ def main():
     if "--big" in sys.argv:
         cases.update(BIG_CASES)
     only = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--cli" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            make_cli(tmp)
+        return
     if "--match" in sys.argv:
         with tempfile.TemporaryDirectory() as tmp:
             make_match(tmp)
