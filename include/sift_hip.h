@@ -235,8 +235,10 @@ int sift_hip_copy_extrema(sift_ctx* ctx, sift_extremum* host_out,
 
 /* Device-side pre-dedup keypoint records of the last detect (n records of
  * sift_kp, unordered): copied device-to-device into `d_dst` (a buffer on the
- * same device) on the context stream, then synchronised. Used by the
- * multi-GPU driver for the RCCL all-gather of descriptor buffers. */
+ * same device), then synchronised. NOTE: these are the kernels' records
+ * before clean_keypoints, and their size field is the device's (ocml pow),
+ * not the final glibc-exact size; sift_hip_fetch_device gives the final,
+ * sorted, de-duplicated records with exact sizes. */
 int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap,
                                  size_t* n_out);
 
