@@ -22,8 +22,13 @@ import os
 import platform
 import sys
 import time
+import collections
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# jobs kept in flight by the pipelined legs: four single-image jobs (one
+# stream each), two 8-image jobs (a stream pair each)
+JOB_DEPTH = max(1, min(8, int(os.environ.get("SIFT_JOB_DEPTH", "4"))))
+BATCH_DEPTH = max(1, min(8, int(os.environ.get("SIFT_BATCH_DEPTH", "2"))))
 sys.path.insert(0, os.path.join(ROOT, "sift-project_amd"))
 
 import numpy as np  # noqa: E402
@@ -141,17 +146,18 @@ def roofline_obj(ms: float, nbytes: float, launches: int, traffic, note) -> dict
     }
 
 
-def pipelined(ctx, submit, n_steps: int):
-    """Run n_steps jobs with job k+1 submitted before job k is fetched;
-    returns (keypoints of all jobs, elapsed s, per-job keypoint counts)."""
+def pipelined(ctx, submit, n_steps: int, depth: int = 0):
+    """Run n_steps jobs with `depth` (default JOB_DEPTH) in flight: job k+d-1
+    is submitted before job k is fetched; returns (keypoints, elapsed s)."""
+    depth = depth or JOB_DEPTH
     kp = 0
     t0 = time.perf_counter()
-    t = submit(0)
+    q = collections.deque()
     for k in range(n_steps):
-        t_next = submit(k + 1) if k + 1 < n_steps else None
-        kps, _ = ctx.fetch(t)
+        while len(q) < depth and k + len(q) < n_steps:
+            q.append(submit(k + len(q)))
+        kps, _ = ctx.fetch(q.popleft())
         kp += sum(len(x) for x in kps)
-        t = t_next
     return kp, time.perf_counter() - t0
 
 
@@ -188,7 +194,7 @@ def extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params, seconds: float) -> d
         "sync_ms_per_image": api * 1e3, "sync_value": kp1 / api,
         "path": "sift_hip_submit/fetch from a host Image buffer (float64 HWC, reference "
                 "image_io.hh:22-26): integer-valued -> packed to u8 on 8 host threads, pinned "
-                "staging, async H2D, u8->f64 on device; pipelined one job ahead (value) and "
+                "staging, async H2D, u8->f64 on device; JOB_DEPTH jobs in flight (value) and "
                 "synchronous per call (sync_*), PCIe included"}
     B = 8
     batch_imgs = [synth_image(W, H, 1, seed=42 + i) for i in range(B)]
@@ -196,14 +202,14 @@ def extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params, seconds: float) -> d
     torch.cuda.synchronize()
     ptrs = [t.data_ptr() for t in bt]
     sub = lambda k: ctx.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params)  # noqa: E731
-    pipelined(ctx, sub, 3)
+    pipelined(ctx, sub, 3, BATCH_DEPTH)
     one = timed_loop(lambda: ctx.fetch(sub(0)), 0.5)
     n_b = max(5, int(seconds / one))
-    kp_b, t_b = pipelined(ctx, sub, n_b)
+    kp_b, t_b = pipelined(ctx, sub, n_b, BATCH_DEPTH)
     out["batch8"] = {"images_per_s": n_b * B / t_b, "ms_per_image": t_b / (n_b * B) * 1e3,
                      "keypoints_per_s": kp_b / t_b, "jobs": n_b,
                      "note": "8 synthetic 1920x1080 images (seeds 42..49) per job, one batched "
-                             "launch per kernel, jobs pipelined one ahead, inputs in HBM"}
+                             "launch per kernel, BATCH_DEPTH jobs in flight, inputs in HBM"}
     out["host_phases_ms"] = phases
     return out
 
@@ -296,17 +302,19 @@ def main() -> int:
             allgather_records([b.to(dev) for b in bufs], ids, B)
         return n_total
 
+    depth = JOB_DEPTH if B == 1 else BATCH_DEPTH
+
     def run(n_steps: int) -> int:
         kp = 0
         if args.sync:
             for _ in range(n_steps):
                 kp += finish(submit())
             return kp
-        t = submit()
+        q = collections.deque()
         for k in range(n_steps):
-            t_next = submit() if k + 1 < n_steps else None
-            kp += finish(t)
-            t = t_next
+            while len(q) < depth and k + len(q) < n_steps:
+                q.append(submit())
+            kp += finish(q.popleft())
         return kp
 
     run(max(1, args.warmup))
@@ -401,6 +409,7 @@ def main() -> int:
                             "reference default parameters",
                 "image": f"{W}x{H}x1",
                 "images_per_gpu_per_step": B,
+                "jobs_in_flight": depth,
                 "keypoints_per_image": kp_per_image,
                 "parallelism": f"image-sharded x{world}" + (
                     ", RCCL all-gather of the descriptor records straight from HBM "

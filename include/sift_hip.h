@@ -147,7 +147,7 @@ const char* sift_hip_strerror(int status);
 #define SIFT_INPUT_U8_HOST 2
 #define SIFT_INPUT_U8_DEVICE 3
 #define SIFT_MAX_BATCH 16
-#define SIFT_MAX_INFLIGHT 2
+#define SIFT_MAX_INFLIGHT 8
 
 /* Enqueue a job; *ticket identifies it. SIFT_ERR_STATE when
  * SIFT_MAX_INFLIGHT jobs are already in flight (wait/fetch one first). */

@@ -21,14 +21,17 @@
 // synchronisation on the pipelined path.
 //
 // Streams. HIP gives a process four hardware queues by default and streams
-// beyond that share a queue and serialise, so a context has exactly four:
-// slot s owns a pyramid stream (high priority) and a keypoint stream (low
-// priority). A job submitted while the other slot has work in flight uses
-// its own pair only, so two jobs never wait on each other (with shared
-// streams the pyramid chains of consecutive jobs serialised and set the
-// step time); a job submitted while the other slot is idle (synchronous use)
-// borrows the other pair too: octaves alternate between both pyramid
-// streams and keypoint batches between both keypoint streams.
+// beyond that share a queue and serialise, so the context's first four
+// streams are two pairs: a pyramid stream (high priority) and a keypoint
+// stream (low priority) each. What a job runs on depends on what is in flight
+// when it is submitted (sift_ctx::pool): alone (synchronous use) it takes
+// all four (octaves alternate between both pyramid streams and keypoint
+// batches between both keypoint streams); next to one other job, the pair
+// that job left free (two jobs never wait on each other; with shared streams
+// the pyramid chains of consecutive jobs serialised and set the step time);
+// next to two or more, one free stream of its own, so four single-image jobs
+// in flight keep four chains on four queues (measured 0.68 vs 0.75 ms per
+// 1080p image at two in flight; BASELINE config 2).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -55,6 +58,7 @@ using clk = std::chrono::steady_clock;
 // the snapshot ranges below stay contiguous).
 constexpr int kLanes = 2;
 constexpr int kSlots = SIFT_MAX_INFLIGHT;
+constexpr int kPairs = 2;
 // device counter block of a slot: [4L..4L+3] live counters of lane L
 // (candidates, refined, records), [8..11] zeros, then per keypoint batch g a
 // 4-word snapshot taken by the last extrema workgroup (the batch's candidate
@@ -192,6 +196,7 @@ struct Slot {
     std::vector<int> chain_lane;
     int n_chains = 0, ev_i = 0;
     size_t ev_used = 0;
+    unsigned uses = 0;  // mask of sift_ctx::pool streams this job runs on
     hipEvent_t done_ev = nullptr;  // lane counters on the host
     // streams of the current job: A, B pyramid (even / odd octaves), C, D
     // keypoint lanes 0 / 1 (A == B and C == D when the job runs alone on its
@@ -231,13 +236,26 @@ struct sift_ctx {
     unsigned kp_wgs = 512;
     int batch_px_log2 = 18;  // octaves of >= 2^this pixels (x images) get their own batch
     size_t tile_max_px = (size_t)1 << 21;  // planes up to this size: LDS-tile blur
+    // octaves of at most this many pixels (and within the LDS, lds_octave_fits)
+    // run LDS-resident in the one-workgroup k_octaves_lds (SIFT_LDS_PX)
+    size_t lds_max_px = kLdsOctavePx;
     bool shared_streams = false;  // SIFT_SHARED_STREAMS=1: every job on all four streams
     bool serial = false;          // SIFT_SERIAL=1: every kernel on one stream (profiling)
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
-    hipStream_t pyr_stream[kSlots] = {};  // slot s: pyramid (high priority)
-    hipStream_t kp_stream[kSlots] = {};   // slot s: keypoint chains (low priority)
+    // two stream pairs, one per hardware queue each (HIP's default is four
+    // queues per process): pair k = pyramid (high priority) + keypoint chains
+    // (low priority)
+    hipStream_t pyr_stream[kPairs] = {};
+    hipStream_t kp_stream[kPairs] = {};
+    // Stream pool: pyr0, pyr1, kp0, kp1, then kSlots - 4 more streams. A job
+    // takes what the jobs in flight leave free (Slot::uses): all four pair
+    // streams when it runs alone, a whole free pair next to one other job,
+    // ONE free stream of its own when two or more are in flight (then up to
+    // kSlots chains share the chip, each on its own hardware queue while
+    // queues last: HIP's default is four per process, GPU_MAX_HW_QUEUES)
+    hipStream_t pool[kSlots] = {};
     int next_ticket = 1;
     int last = -1;  // slot of the last finalised job (introspection)
 
@@ -344,10 +362,12 @@ int ensure_kp_arrays(Slot& s, size_t cand, size_t raw, size_t ori) {
 // After a failure with work already enqueued: let every stream drain before
 // the slot's buffers can be touched again, then free the slot.
 void abandon(sift_ctx* ctx, Slot& s) {
-    for (int k = 0; k < kSlots; ++k) {
+    for (int k = 0; k < kPairs; ++k) {
         (void)hipStreamSynchronize(ctx->pyr_stream[k]);
         (void)hipStreamSynchronize(ctx->kp_stream[k]);
     }
+    for (int k = 2 * kPairs; k < kSlots; ++k)
+        if (ctx->pool[k]) (void)hipStreamSynchronize(ctx->pool[k]);
     s.pending.clear();
     s.state = kFree;
     s.ticket = -1;
@@ -510,7 +530,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // launch (k_octaves_lds); the larger ones get one k_blur launch per level
     int o_small = g.octaves;
     for (int o = 0; o < g.octaves; ++o)
-        if (lds_octave_fits(g.W[o], g.H[o])) {
+        if (lds_octave_fits(g.W[o], g.H[o]) && (size_t)(g.W[o] | 1) * g.H[o] <= ctx->lds_max_px) {
             o_small = o;
             break;
         }
@@ -912,16 +932,35 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     s.ticket = ctx->next_ticket++;
     if (ctx->next_ticket <= 0) ctx->next_ticket = 1;
     {
-        int me = (int)(&s - ctx->slots), other = 1 - me;
-        const bool alone = ctx->shared_streams || ctx->slots[other].state != kSubmitted;
-        if (ctx->shared_streams) me = 0, other = 1;  // A/B: every job on all four
-        s.sA = ctx->pyr_stream[me];
-        s.sC = ctx->kp_stream[me];
-        s.sB = alone ? ctx->pyr_stream[other] : s.sA;
-        s.sD = alone ? ctx->kp_stream[other] : s.sC;
-        s.lanes = alone ? ctx->lanes : 1;
+        int others = 0;
+        unsigned used = 0;
+        for (const Slot& o : ctx->slots)
+            if (&o != &s && o.state == kSubmitted) {
+                ++others;
+                used |= o.uses;
+            }
+        hipStream_t* q = ctx->pool;  // pyr0, pyr1, kp0, kp1, ...
+        if (others == 0 || ctx->shared_streams) {
+            s.sA = q[0], s.sB = q[1], s.sC = q[2], s.sD = q[3];
+            s.lanes = ctx->lanes;
+            s.uses = 0xFu;
+        } else if (others == 1 && !(used & 0x5u)) {
+            s.sA = s.sB = q[0], s.sC = s.sD = q[2];
+            s.lanes = 1;
+            s.uses = 0x5u;
+        } else if (others == 1 && !(used & 0xAu)) {
+            s.sA = s.sB = q[1], s.sC = s.sD = q[3];
+            s.lanes = 1;
+            s.uses = 0xAu;
+        } else {
+            int k = 0;
+            while (k + 1 < kSlots && (used >> k & 1u)) ++k;
+            s.sA = s.sB = s.sC = s.sD = q[k];
+            s.lanes = 1;
+            s.uses = 1u << k;
+        }
         if (ctx->serial) {  // profiling: one stream, no overlap (kernel costs alone)
-            s.sA = s.sB = s.sC = s.sD = ctx->pyr_stream[0];
+            s.sA = s.sB = s.sC = s.sD = q[0];
             s.lanes = 1;
         }
     }
@@ -1024,19 +1063,26 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 18;
     if (const char* e = std::getenv("SIFT_SHARED_STREAMS")) ctx->shared_streams = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_EXTREMA_TILES")) ctx->extrema_stream = std::atoi(e) == 0;
     if (const char* e = std::getenv("SIFT_TILE_PX_LOG2")) {
         const int t = std::atoi(e);  // < 0: never
         ctx->tile_max_px = t < 0 ? 0 : (size_t)1 << std::min(t, 40);
     }
     bool ok = prepare_kernel_attributes() == hipSuccess;
-    for (int k = 0; k < kSlots; ++k)
+    for (int k = 0; k < kPairs; ++k)
         ok = ok &&
              hipStreamCreateWithPriority(&ctx->pyr_stream[k], hipStreamNonBlocking, prio_hi) ==
                  hipSuccess &&
              hipStreamCreateWithPriority(&ctx->kp_stream[k], hipStreamNonBlocking, prio_lo) ==
                  hipSuccess;
     ctx->stream = ctx->pyr_stream[0];
+    ctx->pool[0] = ctx->pyr_stream[0];
+    ctx->pool[1] = ctx->pyr_stream[1];
+    ctx->pool[2] = ctx->kp_stream[0];
+    ctx->pool[3] = ctx->kp_stream[1];
+    for (int k = 2 * kPairs; k < kSlots; ++k)
+        ok = ok && hipStreamCreateWithFlags(&ctx->pool[k], hipStreamNonBlocking) == hipSuccess;
     for (Slot& s : ctx->slots) {
         ok = ok && hipMalloc(&s.d_ctr, kCtrWords * sizeof(unsigned)) == hipSuccess &&
              hipHostMalloc(&s.h_ctr, 4 * kLanes * sizeof(unsigned)) == hipSuccess &&
@@ -1055,10 +1101,12 @@ int sift_hip_create(int device, sift_ctx** out) {
 int sift_hip_destroy(sift_ctx* ctx) {
     if (!ctx) return SIFT_ERR_ARG;
     (void)hipSetDevice(ctx->device);
-    for (int k = 0; k < kSlots; ++k) {
+    for (int k = 0; k < kPairs; ++k) {
         if (ctx->pyr_stream[k]) (void)hipStreamSynchronize(ctx->pyr_stream[k]);
         if (ctx->kp_stream[k]) (void)hipStreamSynchronize(ctx->kp_stream[k]);
     }
+    for (int k = 2 * kPairs; k < kSlots; ++k)
+        if (ctx->pool[k]) (void)hipStreamSynchronize(ctx->pool[k]);
     for (Slot& s : ctx->slots) {
         s.in.release();
         s.in8.release();
@@ -1090,10 +1138,12 @@ int sift_hip_destroy(sift_ctx* ctx) {
     if (ctx->d_mbuf) (void)hipFree(ctx->d_mbuf);
     ctx->h_mj.release();
     ctx->h_md.release();
-    for (int k = 0; k < kSlots; ++k) {
+    for (int k = 0; k < kPairs; ++k) {
         if (ctx->pyr_stream[k]) (void)hipStreamDestroy(ctx->pyr_stream[k]);
         if (ctx->kp_stream[k]) (void)hipStreamDestroy(ctx->kp_stream[k]);
     }
+    for (int k = 2 * kPairs; k < kSlots; ++k)
+        if (ctx->pool[k]) (void)hipStreamDestroy(ctx->pool[k]);
     delete ctx;
     return SIFT_OK;
 }

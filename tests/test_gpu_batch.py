@@ -17,7 +17,8 @@ import pytest
 from golden_util import all_goldens
 from oracle_bind import OracleRun
 from parity import compare_final, final_ok
-from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, INPUT_U8_DEVICE, Context, SiftParams,
+from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, INPUT_U8_DEVICE, MAX_INFLIGHT, Context,
+                      SiftParams,
                       synth_image)
 
 pytestmark = pytest.mark.gpu
@@ -84,14 +85,18 @@ def test_gpu_batch8_1080p_vs_golden_and_oracle(gpu_ctx):
 
 
 def test_gpu_pipelined_jobs(gpu_ctx):
-    """Two jobs in flight; a third submit is refused; out-of-order waits."""
+    """MAX_INFLIGHT jobs in flight; one more submit is refused; out-of-order
+    waits."""
     a = [synth_image(640, 480, 1, seed=s) for s in (1, 2)]
     b = [synth_image(320, 240, 3, seed=3)]
     wa, ha = 640, 480
     ta = gpu_ctx.submit(a, INPUT_F64_HOST, wa, ha, 1)
     tb = gpu_ctx.submit(b, INPUT_F64_HOST, 320, 240, 3)
+    fill = [gpu_ctx.submit(b, INPUT_F64_HOST, 320, 240, 3) for _ in range(MAX_INFLIGHT - 2)]
     with pytest.raises(RuntimeError, match="in flight"):
         gpu_ctx.submit(b, INPUT_F64_HOST, 320, 240, 3)
+    for t in fill:
+        gpu_ctx.fetch(t)
     kb, _ = gpu_ctx.fetch(tb)
     ka, _ = gpu_ctx.fetch(ta)
     _assert_same_records(ka[1], gpu_ctx.detect(a[1])[0])
@@ -105,6 +110,33 @@ def test_gpu_pipelined_jobs(gpu_ctx):
         k, _ = gpu_ctx.fetch(t)
         _assert_same_records(k[0], solo[i - 1])
         t = t_next
+
+
+@pytest.mark.parametrize("depth", [3, 4, 8])
+def test_gpu_deep_pipeline_vs_oracle(gpu_ctx, depth):
+    """`depth` jobs in flight (one stream each beyond two) of
+    mixed shapes and channel counts, fetched in order and one out of order:
+    every job equals the oracle and its synchronous result."""
+    shapes = [(480, 360, 1), (333, 251, 3), (640, 360, 1), (97, 61, 1)]
+    jobs = []
+    for i in range(2 * depth):
+        w, h, c = shapes[i % len(shapes)]
+        jobs.append((synth_image(w, h, c, seed=500 + i), w, h, c))
+    solo = [gpu_ctx.detect(im)[0] for im, *_ in jobs]
+    q = []
+    for i, (im, w, h, c) in enumerate(jobs):
+        if len(q) == depth:
+            j, t = q.pop(0)
+            k, _ = gpu_ctx.fetch(t)
+            _assert_same_records(k[0], solo[j])
+        q.append((i, gpu_ctx.submit([im], INPUT_F64_HOST, w, h, c)))
+    for j, t in reversed(q):  # out of order
+        k, _ = gpu_ctx.fetch(t)
+        _assert_same_records(k[0], solo[j])
+    for j in (0, len(jobs) - 1):
+        ref = OracleRun(jobs[j][0])
+        k, d = gpu_ctx.detect(jobs[j][0], desc_f32=True)
+        assert final_ok(compare_final(k, d, ref.final, ref.desc_f32))
 
 
 def test_gpu_u8_and_device_inputs(gpu_ctx):
