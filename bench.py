@@ -211,7 +211,48 @@ def extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params, seconds: float) -> d
                      "note": "8 synthetic 1920x1080 images (seeds 42..49) per job, one batched "
                              "launch per kernel, BATCH_DEPTH jobs in flight, inputs in HBM"}
     out["host_phases_ms"] = phases
+    out["stitch"] = stitch_leg(ctx, seconds)
     return out
+
+
+def stitch_leg(ctx, seconds: float) -> dict:
+    """the stitching consumer end to end on the GPU
+    (sift_stitch.py: detect every image, GPU match + GPU RANSAC per stitch-graph
+    edge, GPU feather compositing) over the committed 5-image slice of the
+    reference's CAVE-04_times_square dataset, plus the RANSAC scoring kernel
+    alone (hypotheses x point pairs per second)."""
+    from sift_stitch import keypoint_xy, load_dataset, stitch
+
+    graph, images = load_dataset(os.path.join(ROOT, "tests", "golden", "stitch"))
+    res = stitch(ctx, images, graph)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        res = stitch(ctx, images, graph)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds / 2 and n >= 3:
+            break
+    p = res.pairs[0]
+    m = ctx.match(res.keypoints[p.j], res.keypoints[p.i], 0.75)
+    src = keypoint_xy(res.keypoints[p.j])[m["i1"]]
+    dst = keypoint_xy(res.keypoints[p.i])[m["i2"]]
+    n_hyp = 1 << 16
+    ctx.ransac_scores(src, dst, n_hyp=n_hyp)
+    k, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < 0.2 or k < 3:
+        ctx.ransac_scores(src, dst, n_hyp=n_hyp)
+        k += 1
+    dt_r = (time.perf_counter() - t1) / k
+    return {"images": len(images), "edges": len(res.pairs),
+            "ms_per_stitch": dt / n * 1e3, "images_per_s": n * len(images) / dt,
+            "inliers_per_edge": [int(q.inliers) for q in res.pairs],
+            "canvas": list(res.panorama.shape[:2][::-1]),
+            "ransac": {"n_hyp": n_hyp, "pairs": int(len(src)), "ms_per_call": dt_r * 1e3,
+                       "hyp_pairs_per_s": n_hyp * len(src) / dt_r,
+                       "note": "sift_hip_ransac_scores incl. normalisation, upload, score "
+                               "download"},
+            "data": "tests/golden/stitch: CAVE-04_times_square 00-04 (640x480 RGB) and their "
+                    "stitch-graph edges"}
 
 
 def main() -> int:

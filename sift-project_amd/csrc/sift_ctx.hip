@@ -1469,3 +1469,9 @@ int sift_hip_blur_profile(sift_ctx* ctx, double* ms, int64_t* launches, double* 
 }
 
 }  // extern "C"
+
+// the context's public stream, on its device (sift_stitch.hip)
+extern "C" hipStream_t sift_ctx_stream_internal(sift_ctx* ctx) {
+    (void)hipSetDevice(ctx->device);
+    return ctx->stream;
+}

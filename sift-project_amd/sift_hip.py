@@ -84,7 +84,21 @@ EXPORTS = (
     "sift_hip_blur_profile",
     "sift_hip_profile_table",
     "sift_synth_image",
+    "sift_ransac_params_default",
+    "sift_hip_ransac_homography",
+    "sift_hip_ransac_scores",
+    "sift_hip_warp_blend",
 )
+
+
+class CRansacParams(ctypes.Structure):
+    """sift_ransac_params (include/sift_hip.h)."""
+    _fields_ = [
+        ("n_hyp", ctypes.c_int),
+        ("refine_iters", ctypes.c_int),
+        ("threshold", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+    ]
 
 
 class CParams(ctypes.Structure):
@@ -196,6 +210,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                            ctypes.POINTER(ctypes.c_int64), i]
     lib.sift_synth_image.argtypes = [i, i, i, ctypes.c_int64, ctypes.c_double,
                                      ctypes.c_uint64, vp]
+    lib.sift_ransac_params_default.argtypes = [ctypes.POINTER(CRansacParams)]
+    lib.sift_ransac_params_default.restype = None
+    lib.sift_hip_ransac_homography.argtypes = [vp, vp, vp, sz, ctypes.POINTER(CRansacParams), vp,
+                                               vp, ctypes.POINTER(sz)]
+    lib.sift_hip_ransac_scores.argtypes = [vp, vp, vp, sz, ctypes.POINTER(CRansacParams), vp]
+    lib.sift_hip_warp_blend.argtypes = [vp, ctypes.POINTER(vp), vp, vp, i, i, vp, i, i, vp]
     _lib = lib
     return lib
 
@@ -360,6 +380,58 @@ class Context:
                                               ctypes.c_void_p(d_kps2), n2, ratio_threshold,
                                               ctypes.byref(out), ctypes.byref(n)))
         return self._match_result(out, n)
+
+    # ---- stitching consumer (sift_stitch.py drives these) --------------------
+    def ransac_params(self, n_hyp=None, threshold=None, refine_iters=None, seed=None):
+        p = CRansacParams()
+        self.lib.sift_ransac_params_default(ctypes.byref(p))
+        for k, v in (("n_hyp", n_hyp), ("threshold", threshold),
+                     ("refine_iters", refine_iters), ("seed", seed)):
+            if v is not None:
+                setattr(p, k, v)
+        return p
+
+    def ransac_homography(self, src_xy: np.ndarray, dst_xy: np.ndarray, **kw):
+        """(H 3x3 with dst ~ H src, inlier mask, n_inliers) by GPU RANSAC."""
+        a = np.ascontiguousarray(src_xy, dtype=np.float64).reshape(-1, 2)
+        b = np.ascontiguousarray(dst_xy, dtype=np.float64).reshape(-1, 2)
+        if a.shape != b.shape:
+            raise ValueError("src/dst point counts differ")
+        p = self.ransac_params(**kw)
+        H = np.zeros(9, dtype=np.float64)
+        mask = np.zeros(len(a), dtype=np.uint8)
+        n_in = ctypes.c_size_t()
+        _check(self.lib.sift_hip_ransac_homography(self._ctx, a.ctypes.data, b.ctypes.data,
+                                                   len(a), ctypes.byref(p), H.ctypes.data,
+                                                   mask.ctypes.data, ctypes.byref(n_in)))
+        return H.reshape(3, 3), mask.astype(bool), n_in.value
+
+    def ransac_scores(self, src_xy: np.ndarray, dst_xy: np.ndarray, **kw) -> np.ndarray:
+        a = np.ascontiguousarray(src_xy, dtype=np.float64).reshape(-1, 2)
+        b = np.ascontiguousarray(dst_xy, dtype=np.float64).reshape(-1, 2)
+        p = self.ransac_params(**kw)
+        out = np.zeros(p.n_hyp, dtype=np.int32)
+        _check(self.lib.sift_hip_ransac_scores(self._ctx, a.ctypes.data, b.ctypes.data, len(a),
+                                               ctypes.byref(p), out.ctypes.data))
+        return out
+
+    def warp_blend(self, images, Hinv, out_w: int, out_h: int) -> np.ndarray:
+        """Feather-blended panorama (out_h x out_w x c uint8) of HWC uint8
+        images, Hinv[i] = image-from-canvas homography of image i."""
+        ims = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+        ims = [im[:, :, None] if im.ndim == 2 else im for im in ims]
+        c = ims[0].shape[2]
+        if any(im.shape[2] != c for im in ims):
+            raise ValueError("images differ in channel count")
+        ptrs = (ctypes.c_void_p * len(ims))(*[im.ctypes.data for im in ims])
+        w = np.array([im.shape[1] for im in ims], dtype=np.int32)
+        h = np.array([im.shape[0] for im in ims], dtype=np.int32)
+        Hs = np.ascontiguousarray(np.asarray(Hinv, dtype=np.float64).reshape(len(ims), 9))
+        out = np.zeros((out_h, out_w, c), dtype=np.uint8)
+        _check(self.lib.sift_hip_warp_blend(self._ctx, ptrs, w.ctypes.data, h.ctypes.data, c,
+                                            len(ims), Hs.ctypes.data, out_w, out_h,
+                                            out.ctypes.data))
+        return out
 
     def counts(self) -> dict:
         c = CCounts()

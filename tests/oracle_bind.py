@@ -49,6 +49,13 @@ def load_oracle() -> ctypes.CDLL:
     lib.sift_cpu_match.restype = ctypes.c_size_t
     lib.sift_cpu_match.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.c_double,
                                    vp, vp]
+    sz, u64, dbl = ctypes.c_size_t, ctypes.c_uint64, ctypes.c_double
+    lib.sift_cpu_ransac_scores.restype = None
+    lib.sift_cpu_ransac_scores.argtypes = [vp, vp, sz, i, dbl, u64, vp]
+    lib.sift_cpu_ransac_homography.restype = sz
+    lib.sift_cpu_ransac_homography.argtypes = [vp, vp, sz, i, dbl, u64, i, vp, vp]
+    lib.sift_cpu_warp_blend.restype = None
+    lib.sift_cpu_warp_blend.argtypes = [ctypes.POINTER(vp), vp, vp, i, i, vp, i, i, vp]
     _lib = lib
     return lib
 
@@ -130,4 +137,45 @@ def oracle_match(kps1: np.ndarray, kps2: np.ndarray, ratio: float = 0.75) -> np.
     sel = np.nonzero(j[: len(a)] >= 0)[0]
     out = np.zeros(len(sel), dtype=MATCH_DTYPE)
     out["i1"], out["i2"], out["distance"] = sel, j[sel], d[sel]
+    return out
+
+
+# ---- stitching consumer (oracle/stitch_cpu.cpp; parity unpinned vs the
+# reference, whose stitching notebook is absent) -----------------------------
+RANSAC_DEFAULTS = dict(n_hyp=4096, threshold=3.0, seed=0x5EED, refine_iters=2)
+
+
+def _pts(a):
+    return np.ascontiguousarray(a, dtype=np.float64).reshape(-1, 2)
+
+
+def oracle_ransac_scores(src, dst, n_hyp=4096, threshold=3.0, seed=0x5EED) -> np.ndarray:
+    a, b = _pts(src), _pts(dst)
+    out = np.zeros(n_hyp, dtype=np.int32)
+    load_oracle().sift_cpu_ransac_scores(a.ctypes.data, b.ctypes.data, len(a), n_hyp, threshold,
+                                         seed, out.ctypes.data)
+    return out
+
+
+def oracle_ransac_homography(src, dst, n_hyp=4096, threshold=3.0, seed=0x5EED, refine_iters=2):
+    a, b = _pts(src), _pts(dst)
+    H = np.zeros(9, dtype=np.float64)
+    mask = np.zeros(len(a), dtype=np.uint8)
+    k = load_oracle().sift_cpu_ransac_homography(a.ctypes.data, b.ctypes.data, len(a), n_hyp,
+                                                 threshold, seed, refine_iters, H.ctypes.data,
+                                                 mask.ctypes.data)
+    return H.reshape(3, 3), mask.astype(bool), int(k)
+
+
+def oracle_warp_blend(images, Hinv, out_w, out_h) -> np.ndarray:
+    ims = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+    ims = [im[:, :, None] if im.ndim == 2 else im for im in ims]
+    c = ims[0].shape[2]
+    ptrs = (ctypes.c_void_p * len(ims))(*[im.ctypes.data for im in ims])
+    w = np.array([im.shape[1] for im in ims], dtype=np.int32)
+    h = np.array([im.shape[0] for im in ims], dtype=np.int32)
+    Hs = np.ascontiguousarray(np.asarray(Hinv, dtype=np.float64).reshape(len(ims), 9))
+    out = np.zeros((out_h, out_w, c), dtype=np.uint8)
+    load_oracle().sift_cpu_warp_blend(ptrs, w.ctypes.data, h.ctypes.data, c, len(ims),
+                                      Hs.ctypes.data, out_w, out_h, out.ctypes.data)
     return out
