@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "sift_kernels.h"
 
@@ -1537,9 +1538,15 @@ static_assert(kMaxTemplR == 16, "blur tables must cover 1..kMaxTemplR");
 // strips: the small levels are latency-bound).
 BlurShape blur_shape_for(int W, int H, int R) {
     const size_t px = (size_t)W * H;
+    // SIFT_BLUR_ROWS: strip rows on octave-0-sized levels (A/B sweeps)
+    static const int big_rows = [] {
+        const char* e = std::getenv("SIFT_BLUR_ROWS");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 8 && v <= 512 ? v : 32;
+    }();
     BlurShape b;
     b.cols = (!(W & 1) && px >= ((size_t)1 << 20)) ? 2 : 1;
-    b.rows = px >= ((size_t)4 << 20) ? 32 : 16;
+    b.rows = px >= ((size_t)4 << 20) ? big_rows : 16;
     if (R > 12 && b.cols == 2) b.rows = 16;
     if (b.rows > H) b.rows = H;
     return b;
