@@ -146,6 +146,46 @@ def roofline_obj(ms: float, nbytes: float, launches: int, traffic, note) -> dict
     }
 
 
+def alone_leg(dev_img, W, H, params, n_images: int = 200) -> dict:
+    """Kernel-quality view of the same launches: a second context with
+    SIFT_SERIAL=1 runs every kernel of a detect on one stream, so each launch
+    has the chip to itself (no other job's kernels share the CUs). The timed
+    region's roofline above is the pipelined one, where four jobs' chains
+    share the chip and every launch lasts longer while the job rate rises."""
+    os.environ["SIFT_SERIAL"] = "1"
+    try:
+        sctx = Context(torch.cuda.current_device())
+    finally:
+        del os.environ["SIFT_SERIAL"]
+    for _ in range(10):
+        sctx.detect_device(dev_img.data_ptr(), W, H, 1, params)
+    sctx.set_profiling(True)
+    sctx.profile_table(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(n_images):
+        sctx.detect_device(dev_img.data_ptr(), W, H, 1, params)
+    dt = time.perf_counter() - t0
+    sctx.set_profiling(False)
+    prof = sctx.profile_table(reset=True)
+    sctx.close()
+    rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
+    ms, nb, n = (sum(r[k] for r in rows) for k in range(3))
+    pyr = roofline_obj(ms, nb, n, None, None)
+    pyr["us_per_image"] = ms * 1e3 / n_images
+    pyr["per_octave"] = [{"octave": o, "us_per_launch": m * 1e3 / k,
+                          "achieved_GBps": b / (m * 1e-3) / 1e9}
+                         for o, (m, b, k) in enumerate(rows) if k]
+    ems, eb, en = prof[PROF_EXTREMA]
+    ext = roofline_obj(ems, eb, en, None, None)
+    ext["us_per_image"] = ems * 1e3 / n_images
+    for d in (pyr, ext):
+        for k in ("traffic", "traffic_source", "traffic_over_algorithmic"):
+            d.pop(k)
+    note = (f"SIFT_SERIAL=1 context, {n_images} synchronous detects of the same image, every "
+            f"kernel alone on the chip; {dt / n_images * 1e3:.3f} ms per image serialised")
+    return {"pyramid": pyr, "extrema": ext, "note": note}
+
+
 def pipelined(ctx, submit, n_steps: int, depth: int = 0):
     """Run n_steps jobs with `depth` (default JOB_DEPTH) in flight: job k+d-1
     is submitted before job k is fetched; returns (keypoints, elapsed s)."""
@@ -460,6 +500,11 @@ def main() -> int:
             "extrema_roofline": extrema_roofline,
         }
         out["timed_region_s"] = elapsed
+        if world == 1 and not args.no_events:
+            alone = alone_leg(dev_imgs[0], W, H, params)
+            roofline["alone"] = alone["pyramid"]
+            roofline["alone"]["note"] = alone["note"]
+            extrema_roofline["alone"] = alone["extrema"]
         if exchange_check is not None:
             out["exchange_check"] = exchange_check
         if world == 1 and not args.no_extra:

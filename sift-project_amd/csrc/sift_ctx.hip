@@ -242,6 +242,8 @@ struct sift_ctx {
     bool shared_streams = false;  // SIFT_SHARED_STREAMS=1: every job on all four streams
     bool serial = false;          // SIFT_SERIAL=1: every kernel on one stream (profiling)
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
+    bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
+    int desc_mode = 1;            // SIFT_DESC_MODE: k_descriptor variant (0 f64, 1 f32 math, 2 f32 hist)
     int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
     // two stream pairs, one per hardware queue each (HIP's default is four
@@ -501,7 +503,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             SIFT_OK)
             return SIFT_ERR_HIP;
         hipError_t err = hipSuccess;
-        const bool fused = launch_blur_initial_fused(src, in_bs, s.w, s.h, s.c,
+        const bool fused = ctx->fuse_initial &&
+                           launch_blur_initial_fused(src, in_bs, s.w, s.h, s.c,
                                                      p->double_image_size ? 1 : 0,
                                                      s.h_pt.lvl[0][0], stride, n_img, W0, H0,
                                                      s.taps_init, sA, e0, e1, &err);
@@ -613,7 +616,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
                                    cap_ori, work, ctx->kp_wgs, sx));
         SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
-                                       work + 2, ex, ctx->kp_wgs, sx));
+                                       work + 2, ex, ctx->kp_wgs, ctx->desc_mode, sx));
         SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], sx));
         return SIFT_OK;
     };
@@ -757,7 +760,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
                                        s.side.p, live + 2, cap_ori, work, ctx->kp_wgs, sC));
             SIFT_HIP_TRY(launch_descriptor(d_pt, s.dp, s.ori.p, s.side.p, zeros, live + 2, cap_ori,
                                            s.want_df ? s.df32.p : nullptr, work + 2, ex,
-                                           ctx->kp_wgs, sC));
+                                           ctx->kp_wgs, ctx->desc_mode, sC));
             SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
             SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
@@ -1063,6 +1066,8 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 18;
     if (const char* e = std::getenv("SIFT_SHARED_STREAMS")) ctx->shared_streams = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
+    if (const char* e = std::getenv("SIFT_FUSE_INITIAL")) ctx->fuse_initial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_EXTREMA_TILES")) ctx->extrema_stream = std::atoi(e) == 0;
     if (const char* e = std::getenv("SIFT_TILE_PX_LOG2")) {

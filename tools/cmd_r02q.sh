@@ -1,0 +1,10 @@
+set -o pipefail
+R=$(pwd)
+O=$R/gpurun_out/r02q
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+SWEEP="base" REPS=2 SWEEP_OUT=r02q/sw.txt tools/sweep.sh | grep mean || exit 1
+cd /tmp && export TMPDIR=/tmp
+SIFT_SERIAL=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/ser -o run -- python3 $R/bench.py --sync --steps 200 --warmup 10 --no-cpu-baseline --no-extra --no-matcher --no-events > $O/ser.json 2> $O/ser.err || { tail -5 $O/ser.err; exit 1; }
+cat $O/ser/run_kernel_stats.csv | cut -d, -f1-5 | head -12
