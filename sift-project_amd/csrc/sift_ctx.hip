@@ -329,7 +329,11 @@ ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img, b
         // (2 priming rows per segment), at most 64
         int ch = 16;
         if (stream) {
-            const long rows = (long)tx * std::max(g.H[o] - 2, 0) * n_img / 4096;
+            static const long waves = [] {  // SIFT_EXT_WAVES: A/B knob
+                const char* e = std::getenv("SIFT_EXT_WAVES");
+                return e ? std::max(64L, std::atol(e)) : 4096L;
+            }();
+            const long rows = (long)tx * std::max(g.H[o] - 2, 0) * n_img / waves;
             ch = (int)std::min<long>(64, std::max<long>(4, rows));
         }
         const int ty = g.H[o] > 2 ? (g.H[o] - 2 + ch - 1) / ch : 0;

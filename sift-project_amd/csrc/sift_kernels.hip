@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -24,6 +25,12 @@
 // compile-time A/B knobs (alternative builds, SIFT_HIP_LIB)
 #ifndef SIFT_BLUR_PF
 #define SIFT_BLUR_PF 2  // k_blur: source rows in flight ahead of the staged one
+#endif
+#ifndef SIFT_DESC_AHEAD
+#define SIFT_DESC_AHEAD 1  // k_descriptor: samples (x64) whose loads are in flight
+#endif
+#ifndef SIFT_DESC_OCC
+#define SIFT_DESC_OCC 5  // k_descriptor (f32 math): min workgroups per CU
 #endif
 #ifndef SIFT_EXT_PF
 #define SIFT_EXT_PF 2  // k_extrema_stream: rows in flight
@@ -84,7 +91,9 @@ __device__ __forceinline__ void xcd_remap(int& bx, int& by, int& bz) {
 // input: convert_to_grayscale (image.cpp:8-24) and, with double_image_size,
 // resize_inter_bilinear x2 (image.cpp:62-88); bit-identical to materialising
 // it first (same expressions, evaluated once per staged pixel).
-enum BlurSrcMode { kSrcPlane = 0, kSrcGray = 1, kSrcUpsample = 2 };
+// kSrcUpsample: one-channel input, kSrcUpsampleRGB: three channels (the
+// raw input ring holds 1 or 3 values per column and row)
+enum BlurSrcMode { kSrcPlane = 0, kSrcGray = 1, kSrcUpsample = 2, kSrcUpsampleRGB = 3 };
 
 template <int MODE>
 __device__ __forceinline__ double fetch_src(const BlurSource& s, int W, int yy, int gx) {
@@ -213,11 +222,71 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
         for (int q = 0; q < NW; ++q) win[c][q] = 0.0;
     const int yy0 = y_begin - R, yy_last = y_end + R;  // inclusive: one drain step
     double pf[PF][NL];
+    constexpr bool UP = MODE == kSrcUpsample || MODE == kSrcUpsampleRGB;
+    if (!UP) {
 #pragma unroll
-    for (int p = 0; p < PF; ++p) {
-        const int ry = clampi(yy0 + p, 0, H - 1);
+        for (int p = 0; p < PF; ++p) {
+            const int ry = clampi(yy0 + p, 0, H - 1);
 #pragma unroll
-        for (int q = 0; q < NL; ++q) pf[p][q] = fetch_src<MODE>(src, W, ry, gx[q]);
+            for (int q = 0; q < NL; ++q) pf[p][q] = fetch_src<MODE>(src, W, ry, gx[q]);
+        }
+    }
+    // kSrcUpsample (resize_inter_bilinear x2 of the gray input, image.cpp:
+    // 62-88): staged row ry interpolates input rows y0 = ry/2 and
+    // y1 = min(y0 + 1, h - 1) with dy in {0, 0.5}. Instead of 4 gathers per
+    // staged pixel, a ring of input rows follows the walk: hx0 / hx1 hold the
+    // horizontally interpolated rows y0 and y1 (v0, v1 of the reference), two
+    // more rows are in flight as raw input (kUpAhead rows ahead), and each
+    // input row is loaded once per strip. Same expressions, same operands:
+    // bit-identical to fetch_src<kSrcUpsample>.
+    constexpr int kUpAhead = 2;  // raw slots 0, 1
+    constexpr int UC = (MODE == kSrcUpsampleRGB) ? 3 : 1;  // raw channel slots
+    int ux0[NL], ux1[NL];
+    double udx[NL], hx0[NL], hx1[NL], raw[kUpAhead][NL][2 * UC];
+    int ci = 0;  // input row of hx0 (hx1: min(ci + 1, h - 1))
+    // raw slot a <- input row r (clamped); hx <- gray + horizontal
+    // interpolation of raw slot a: v = g0 * (1 - dx) + g1 * dx
+#define SIFT_UP_LOAD(r, a)                                                             \
+    {                                                                                  \
+        const double* row_ = src.p + (size_t)min((r), src.h - 1) * src.w * src.c;    \
+        _Pragma("unroll") for (int q = 0; q < NL; ++q) {                               \
+            if (UC == 1 || src.c == 1) {                                               \
+                raw[a][q][0] = row_[(size_t)ux0[q] * src.c];                           \
+                raw[a][q][1] = row_[(size_t)ux1[q] * src.c];                           \
+            } else {                                                                   \
+                _Pragma("unroll") for (int ch = 0; ch < UC; ++ch) {                    \
+                    raw[a][q][2 * ch] = row_[(size_t)ux0[q] * src.c + ch];             \
+                    raw[a][q][2 * ch + 1] = row_[(size_t)ux1[q] * src.c + ch];         \
+                }                                                                      \
+            }                                                                          \
+        }                                                                              \
+    }
+#define SIFT_UP_HX(a, hx)                                                              \
+    {                                                                                  \
+        _Pragma("unroll") for (int q = 0; q < NL; ++q) {                               \
+            double g0 = raw[a][q][0], g1 = raw[a][q][1];                               \
+            if (UC == 3 && src.c != 1) {                                               \
+                g0 = 0.2126 * raw[a][q][0] + 0.7152 * raw[a][q][2] + 0.0722 * raw[a][q][4]; \
+                g1 = 0.2126 * raw[a][q][1] + 0.7152 * raw[a][q][3] + 0.0722 * raw[a][q][5]; \
+            }                                                                          \
+            hx[q] = g0 * (1 - udx[q]) + g1 * udx[q];                                   \
+        }                                                                              \
+    }
+    if (UP) {
+#pragma unroll
+        for (int q = 0; q < NL; ++q) {
+            const double fx = gx[q] / 2.0;
+            ux0[q] = (int)fx;
+            ux1[q] = min(ux0[q] + 1, src.w - 1);
+            udx[q] = fx - ux0[q];
+        }
+        ci = clampi(yy0, 0, H - 1) >> 1;
+        SIFT_UP_LOAD(ci, 0)
+        SIFT_UP_HX(0, hx0)
+        SIFT_UP_LOAD(ci + 1, 0)
+        SIFT_UP_HX(0, hx1)
+        SIFT_UP_LOAD(ci + 2, 0)
+        SIFT_UP_LOAD(ci + 3, 1)
     }
     const int xa = x0 + C * lane;
     for (int yb = yy0; yb <= yy_last; yb += NW) {
@@ -225,13 +294,30 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
         for (int s = 0; s < NW; ++s) {
             const int yy = yb + s;
             if (yy <= yy_last) {
+                if (UP) {
+                    const int ry = clampi(yy, 0, H - 1);
+                    if ((ry >> 1) > ci) {  // advance the ring by one input row
 #pragma unroll
-                for (int q = 0; q < NL; ++q) sl[lane + 64 * q] = pf[0][q];
+                        for (int q = 0; q < NL; ++q) hx0[q] = hx1[q];
+                        SIFT_UP_HX(0, hx1)
 #pragma unroll
-                for (int p = 0; p + 1 < PF; ++p)
+                        for (int q = 0; q < NL; ++q)
 #pragma unroll
-                    for (int q = 0; q < NL; ++q) pf[p][q] = pf[p + 1][q];
-                {
+                            for (int e = 0; e < 2 * UC; ++e) raw[0][q][e] = raw[1][q][e];
+                        SIFT_UP_LOAD(ci + 2 + kUpAhead, 1)
+                        ++ci;
+                    }
+                    const double dy = (ry & 1) ? 0.5 : 0.0;  // ry / 2.0 - (int)(ry / 2.0)
+#pragma unroll
+                    for (int q = 0; q < NL; ++q)
+                        sl[lane + 64 * q] = hx0[q] * (1 - dy) + hx1[q] * dy;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < NL; ++q) sl[lane + 64 * q] = pf[0][q];
+#pragma unroll
+                    for (int p = 0; p + 1 < PF; ++p)
+#pragma unroll
+                        for (int q = 0; q < NL; ++q) pf[p][q] = pf[p + 1][q];
                     const int ry = clampi(yy + PF, 0, H - 1);
 #pragma unroll
                     for (int q = 0; q < NL; ++q) pf[PF - 1][q] = fetch_src<MODE>(src, W, ry, gx[q]);
@@ -293,6 +379,9 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
         }
     }
 }
+
+#undef SIFT_UP_LOAD
+#undef SIFT_UP_HX
 
 // ---------------------------------------------------------------------------
 // k_blur_tile<R, DECIM>: the same level (image.cpp:156-214) for planes small
@@ -444,8 +533,13 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
         const int y = task - (x0 / kLdsRun) * H;
         const double* row = L.A + y * P;
         double v[NV];
+        if (x0 >= R && x0 + kLdsRun + R <= W) {  // interior run: no clamping
 #pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = row[clampi(x0 - R + i, 0, W - 1)];
+            for (int i = 0; i < NV; ++i) v[i] = row[x0 - R + i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) v[i] = row[clampi(x0 - R + i, 0, W - 1)];
+        }
         double acc[kLdsRun];
 #pragma unroll
         for (int j = 0; j < kLdsRun; ++j) acc[j] = v[j + R] * k[0];
@@ -466,8 +560,14 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
         const int x = task - yr * W;
         const int y0 = yr * kLdsRun;
         double v[NV];
+        if (y0 >= R && y0 + kLdsRun + R <= H) {  // interior run: no clamping
+            const double* col = L.T + (y0 - R) * P + x;
 #pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = L.T[clampi(y0 - R + i, 0, H - 1) * P + x];
+            for (int i = 0; i < NV; ++i) v[i] = col[i * P];
+        } else {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) v[i] = L.T[clampi(y0 - R + i, 0, H - 1) * P + x];
+        }
         double acc[kLdsRun];
 #pragma unroll
         for (int j = 0; j < kLdsRun; ++j) acc[j] = v[j + R] * k[0];
@@ -1254,17 +1354,31 @@ __device__ void describe(DescLdsT<MODE>& S, const PyrTable* __restrict__ pt, con
                 v[3] = img[r0 + W];
             }
         };
-        // one sample ahead: the next sample's four gradient loads are in
+        // kAhead samples ahead: the next samples' gradient loads are in
         // flight while the current one is processed
+        constexpr int kAhead = SIFT_DESC_AHEAD;
         int srow = 0, scol = 0;
-        double cv[4] = {0.0, 0.0, 0.0, 0.0}, nv[4] = {0.0, 0.0, 0.0, 0.0};
+        double cv[4] = {0.0, 0.0, 0.0, 0.0};
         bool cok = total > 0 && locate(0, srow, scol);
         fetch(cok, srow, scol, cv);
+        int qrow[kAhead], qcol[kAhead];
+        bool qok[kAhead];
+        double qv[kAhead][4];
+#pragma unroll
+        for (int a = 0; a + 1 < kAhead; ++a) {
+            qrow[a] = qcol[a] = 0;
+            qok[a] = false;
+            if (64 * (a + 1) < total) qok[a] = locate(64 * (a + 1), qrow[a], qcol[a]);
+            fetch(qok[a], qrow[a], qcol[a], qv[a]);
+        }
         for (int t0 = 0; t0 < total; t0 += 64) {
-            int nrow = 0, ncol = 0;
-            bool nok = false;
-            if (t0 + 64 < total) nok = locate(t0 + 64, nrow, ncol);
-            fetch(nok, nrow, ncol, nv);
+            int& nrow = qrow[kAhead - 1];
+            int& ncol = qcol[kAhead - 1];
+            bool& nok = qok[kAhead - 1];
+            nrow = ncol = 0;
+            nok = false;
+            if (t0 + 64 * kAhead < total) nok = locate(t0 + 64 * kAhead, nrow, ncol);
+            fetch(nok, nrow, ncol, qv[kAhead - 1]);
             if (F32 && cok) {
                 const float fcol = (float)scol, frow = (float)srow;
                 const float row_rot = fmaf(fcol, saf, frow * caf) * ihwf;
@@ -1341,11 +1455,19 @@ __device__ void describe(DescLdsT<MODE>& S, const PyrTable* __restrict__ pt, con
                     }
                 }
             }
-            srow = nrow;
-            scol = ncol;
+            srow = qrow[0];
+            scol = qcol[0];
+            cok = qok[0];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
-            cok = nok;
+            for (int q = 0; q < 4; ++q) cv[q] = qv[0][q];
+#pragma unroll
+            for (int a = 0; a + 1 < kAhead; ++a) {
+                qrow[a] = qrow[a + 1];
+                qcol[a] = qcol[a + 1];
+                qok[a] = qok[a + 1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
+            }
         }
     }
     __syncthreads();
@@ -1606,7 +1728,7 @@ __global__ __launch_bounds__(256, 4) void k_orient(
 // Descriptors of records [*rec_begin, *n_rec), one workgroup per record
 // from a work counter; workgroup 0 publishes the range.
 template <int MODE>
-__global__ __launch_bounds__(256, MODE == 0 ? 3 : (MODE == 1 ? 5 : 4)) void k_descriptor(const PyrTable* __restrict__ pt, DevParams P,
+__global__ __launch_bounds__(256, MODE == 0 ? 3 : (MODE == 1 ? SIFT_DESC_OCC : 4)) void k_descriptor(const PyrTable* __restrict__ pt, DevParams P,
                                                     sift_kp* __restrict__ recs,
                                                     const RecSide* __restrict__ rec_side,
                                                     const unsigned* __restrict__ rec_begin,
@@ -1680,6 +1802,8 @@ using BlurGray1 = BlurTable<1, kSrcGray, SIFT_R_LIST>;
 using BlurGray2 = BlurTable<2, kSrcGray, SIFT_R_LIST>;
 using BlurUps1 = BlurTable<1, kSrcUpsample, SIFT_R_LIST>;
 using BlurUps2 = BlurTable<2, kSrcUpsample, SIFT_R_LIST>;
+using BlurUpsRGB1 = BlurTable<1, kSrcUpsampleRGB, SIFT_R_LIST>;
+using BlurUpsRGB2 = BlurTable<2, kSrcUpsampleRGB, SIFT_R_LIST>;
 #undef SIFT_R_LIST
 static_assert(kMaxTemplR == 16, "blur tables must cover 1..kMaxTemplR");
 
@@ -1714,8 +1838,10 @@ static hipError_t launch_blur_shaped(int MODE, const BlurSource& bs, double* dst
         f = sh.cols == 2 ? BlurPlane2::fns[i] : BlurPlane1::fns[i];
     else if (MODE == kSrcGray)
         f = sh.cols == 2 ? BlurGray2::fns[i] : BlurGray1::fns[i];
-    else
+    else if (MODE == kSrcUpsample)
         f = sh.cols == 2 ? BlurUps2::fns[i] : BlurUps1::fns[i];
+    else
+        f = sh.cols == 2 ? BlurUpsRGB2::fns[i] : BlurUpsRGB1::fns[i];
     return f(bs, dst, dst_bs, n_img, W, H, sh.rows, taps, dec, Wd, Hd, s, e0, e1);
 }
 
@@ -1776,7 +1902,7 @@ bool launch_blur_initial_fused(const double* in, size_t in_bs, int w, int h, int
     const int R = taps.R;
     if (R < 1 || R > kMaxTemplR || (c == 1 && !dbl)) return false;
     const BlurSource src_desc{in, in_bs, w, h, c};
-    *err = launch_blur_shaped(dbl ? kSrcUpsample : kSrcGray, src_desc, dst, bs, n_img, W0, H0,
+    *err = launch_blur_shaped(dbl ? (c == 1 ? kSrcUpsample : kSrcUpsampleRGB) : kSrcGray, src_desc, dst, bs, n_img, W0, H0,
                               taps, nullptr, 0, 0, s, e0, e1);
     return true;
 }
@@ -1929,8 +2055,12 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_i
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s) {
+    static const unsigned max_blocks = [] {  // SIFT_REFINE_WGS: A/B knob
+        const char* e = std::getenv("SIFT_REFINE_WGS");
+        return e ? (unsigned)std::max(1, std::atoi(e)) : 1024u;
+    }();
     unsigned blocks = (cap_cand + 255) / 256;
-    if (blocks > 1024) blocks = 1024;
+    if (blocks > max_blocks) blocks = max_blocks;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(k_refine, dim3(blocks), dim3(256), 0, s, d_pt, P, cand, cand_begin, n_cand,
                        cap_cand, out, n_out, cap_out);

@@ -157,14 +157,14 @@ class SiftParams:
         return p
 
 
-_lib = None
+_libs: dict = {}
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libsift_hip.so (raises if it has not been built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
+    """Load libsift_hip.so (raises if it has not been built). Other paths
+    (alternative builds for A/B runs) load side by side (RTLD_LOCAL)."""
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise RuntimeError(
             f"{path} not found: build it with `make -C sift-project_amd` "
@@ -216,7 +216,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                                vp, ctypes.POINTER(sz)]
     lib.sift_hip_ransac_scores.argtypes = [vp, vp, vp, sz, ctypes.POINTER(CRansacParams), vp]
     lib.sift_hip_warp_blend.argtypes = [vp, ctypes.POINTER(vp), vp, vp, i, i, vp, i, i, vp]
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -249,8 +249,8 @@ def _as_hwc(img: np.ndarray):
 class Context:
     """One HIP device context (stream + device arena)."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load_library()
+    def __init__(self, device: int = 0, lib_path: str | None = None):
+        self.lib = load_library(lib_path or LIB_PATH)
         self._ctx = ctypes.c_void_p()
         _check(self.lib.sift_hip_create(device, ctypes.byref(self._ctx)))
         self.device = device
