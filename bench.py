@@ -146,7 +146,24 @@ def roofline_obj(ms: float, nbytes: float, launches: int, traffic, note) -> dict
     }
 
 
-def alone_leg(dev_img, W, H, params, n_images: int = 200) -> dict:
+def _rows_roofline(prof, n_images):
+    rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
+    ms, nb, n = (sum(r[k] for r in rows) for k in range(3))
+    pyr = roofline_obj(ms, nb, n, None, None)
+    pyr["us_per_image"] = ms * 1e3 / n_images
+    pyr["per_octave"] = [{"octave": o, "us_per_launch": m * 1e3 / k,
+                          "achieved_GBps": b / (m * 1e-3) / 1e9}
+                         for o, (m, b, k) in enumerate(rows) if k]
+    ems, eb, en = prof[PROF_EXTREMA]
+    ext = roofline_obj(ems, eb, en, None, None)
+    ext["us_per_image"] = ems * 1e3 / n_images
+    for d in (pyr, ext):
+        for k in ("traffic", "traffic_source", "traffic_over_algorithmic"):
+            d.pop(k)
+    return pyr, ext
+
+
+def alone_leg(dev_img, W, H, params, n_images: int = 200, batch_imgs=None) -> dict:
     """Kernel-quality view of the same launches: a second context with
     SIFT_SERIAL=1 runs every kernel of a detect on one stream, so each launch
     has the chip to itself (no other job's kernels share the CUs). The timed
@@ -166,24 +183,27 @@ def alone_leg(dev_img, W, H, params, n_images: int = 200) -> dict:
         sctx.detect_device(dev_img.data_ptr(), W, H, 1, params)
     dt = time.perf_counter() - t0
     sctx.set_profiling(False)
-    prof = sctx.profile_table(reset=True)
-    sctx.close()
-    rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
-    ms, nb, n = (sum(r[k] for r in rows) for k in range(3))
-    pyr = roofline_obj(ms, nb, n, None, None)
-    pyr["us_per_image"] = ms * 1e3 / n_images
-    pyr["per_octave"] = [{"octave": o, "us_per_launch": m * 1e3 / k,
-                          "achieved_GBps": b / (m * 1e-3) / 1e9}
-                         for o, (m, b, k) in enumerate(rows) if k]
-    ems, eb, en = prof[PROF_EXTREMA]
-    ext = roofline_obj(ems, eb, en, None, None)
-    ext["us_per_image"] = ems * 1e3 / n_images
-    for d in (pyr, ext):
-        for k in ("traffic", "traffic_source", "traffic_over_algorithmic"):
-            d.pop(k)
+    pyr, ext = _rows_roofline(sctx.profile_table(reset=True), n_images)
     note = (f"SIFT_SERIAL=1 context, {n_images} synchronous detects of the same image, every "
             f"kernel alone on the chip; {dt / n_images * 1e3:.3f} ms per image serialised")
-    return {"pyramid": pyr, "extrema": ext, "note": note}
+    out = {"pyramid": pyr, "extrema": ext, "note": note}
+    if batch_imgs:
+        # BASELINE config 4's per-GPU share: one 8-image job per launch, alone
+        ptrs = [t.data_ptr() for t in batch_imgs]
+        nb_jobs = max(3, n_images // (4 * len(ptrs)))
+        for _ in range(2):
+            sctx.fetch(sctx.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params))
+        sctx.set_profiling(True)
+        sctx.profile_table(reset=True)
+        for _ in range(nb_jobs):
+            sctx.fetch(sctx.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params))
+        sctx.set_profiling(False)
+        bp, be = _rows_roofline(sctx.profile_table(reset=True), nb_jobs * len(ptrs))
+        out["batch"] = {"pyramid": bp, "extrema": be,
+                        "note": f"{nb_jobs} jobs of {len(ptrs)} 1920x1080 images (one launch per "
+                                f"kernel covers the job), SIFT_SERIAL=1 context"}
+    sctx.close()
+    return out
 
 
 def pipelined(ctx, submit, n_steps: int, depth: int = 0):
@@ -501,10 +521,15 @@ def main() -> int:
         }
         out["timed_region_s"] = elapsed
         if world == 1 and not args.no_events:
-            alone = alone_leg(dev_imgs[0], W, H, params)
+            b8 = [torch.from_numpy(synth_image(W, H, 1, seed=42 + i)).to(dev) for i in range(8)]
+            alone = alone_leg(dev_imgs[0], W, H, params, batch_imgs=b8)
+            del b8
             roofline["alone"] = alone["pyramid"]
             roofline["alone"]["note"] = alone["note"]
             extrema_roofline["alone"] = alone["extrema"]
+            roofline["alone_batch8"] = alone["batch"]["pyramid"]
+            roofline["alone_batch8"]["note"] = alone["batch"]["note"]
+            extrema_roofline["alone_batch8"] = alone["batch"]["extrema"]
         if exchange_check is not None:
             out["exchange_check"] = exchange_check
         if world == 1 and not args.no_extra:

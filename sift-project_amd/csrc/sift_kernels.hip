@@ -406,10 +406,14 @@ __global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ sr
                                                    double* __restrict__ dec, int Wd, int Hd) {
     constexpr int SH = kTileH + 2 * R;             // staged rows
     constexpr int SWp = (kTileW + 2 * R) | 1;      // staged row stride (odd)
-    constexpr int TWp = kTileW + 1;                // row-pass row stride (odd)
     constexpr int RX = 4, RY = 8;                  // output runs per task
+    // one LDS region: the staged source, overwritten in place by the row
+    // pass (results held in registers across a barrier), so a tile workgroup
+    // takes 23-35 KB instead of 44-62 KB and more of them (and of other jobs'
+    // kernels) fit on a CU
     __shared__ double sin_[SH * SWp];
-    __shared__ double tmp[SH * TWp];
+    double* const tmp = sin_;
+    constexpr int TS = SWp;  // row-pass row stride (odd)
     const int tid = threadIdx.x;
     int bx, by, bz;
     xcd_remap(bx, by, bz);
@@ -443,21 +447,37 @@ __global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ sr
     __syncthreads();
     // row pass (image.cpp:170-185): task = (row r, columns c0..c0+RX-1);
     // consecutive lanes take consecutive rows
-    for (int t = tid; t < SH * (kTileW / RX); t += 256) {
-        const int r = t % SH, c0 = (t / SH) * RX;
-        const double* row = sin_ + r * SWp + c0;
-        double v[RX + 2 * R];
+    constexpr int NTASK = SH * (kTileW / RX);
+    constexpr int NT = (NTASK + 255) / 256;
+    double res[NT][RX];
 #pragma unroll
-        for (int j = 0; j < RX + 2 * R; ++j) v[j] = row[j];
-        double acc[RX];
+    for (int it = 0; it < NT; ++it) {
+        const int t = tid + 256 * it;
+        if (t < NTASK) {
+            const int r = t % SH, c0 = (t / SH) * RX;
+            const double* row = sin_ + r * SWp + c0;
+            double v[RX + 2 * R];
 #pragma unroll
-        for (int j = 0; j < RX; ++j) acc[j] = v[j + R] * k[0];
+            for (int j = 0; j < RX + 2 * R; ++j) v[j] = row[j];
 #pragma unroll
-        for (int u = 1; u <= R; ++u)
+            for (int j = 0; j < RX; ++j) res[it][j] = v[j + R] * k[0];
 #pragma unroll
-            for (int j = 0; j < RX; ++j) acc[j] += k[u] * (v[j + R + u] + v[j + R - u]);
+            for (int u = 1; u <= R; ++u)
 #pragma unroll
-        for (int j = 0; j < RX; ++j) tmp[r * TWp + c0 + j] = div_sum_w(acc[j], sw, inv);
+                for (int j = 0; j < RX; ++j) res[it][j] += k[u] * (v[j + R + u] + v[j + R - u]);
+#pragma unroll
+            for (int j = 0; j < RX; ++j) res[it][j] = div_sum_w(res[it][j], sw, inv);
+        }
+    }
+    __syncthreads();  // every staged value has been read
+#pragma unroll
+    for (int it = 0; it < NT; ++it) {
+        const int t = tid + 256 * it;
+        if (t < NTASK) {
+            const int r = t % SH, c0 = (t / SH) * RX;
+#pragma unroll
+            for (int j = 0; j < RX; ++j) tmp[r * TS + c0 + j] = res[it][j];
+        }
     }
     __syncthreads();
     // column pass (image.cpp:193-208): task = (column c, rows r0..r0+RY-1)
@@ -465,7 +485,7 @@ __global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ sr
         const int c = tid % kTileW, r0 = (tid / kTileW) * RY;
         double v[RY + 2 * R];
 #pragma unroll
-        for (int j = 0; j < RY + 2 * R; ++j) v[j] = tmp[(r0 + j) * TWp + c];
+        for (int j = 0; j < RY + 2 * R; ++j) v[j] = tmp[(r0 + j) * TS + c];
         double acc[RY];
 #pragma unroll
         for (int j = 0; j < RY; ++j) acc[j] = v[j + R] * k[0];
