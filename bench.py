@@ -342,6 +342,9 @@ def main() -> int:
     ap.add_argument("--extra-seconds", type=float, default=2.0)
     ap.add_argument("--no-events", action="store_true",
                     help="skip the per-launch HIP events of the pyramid roofline")
+    ap.add_argument("--no-alone", action="store_true",
+                    help="skip the kernel-alone roofline legs (PMC sessions count only the "
+                         "timed region's launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py); used only "
                          "while its kernel-source hash matches the sources")
@@ -520,7 +523,7 @@ def main() -> int:
             "extrema_roofline": extrema_roofline,
         }
         out["timed_region_s"] = elapsed
-        if world == 1 and not args.no_events:
+        if world == 1 and not args.no_events and not args.no_alone:
             b8 = [torch.from_numpy(synth_image(W, H, 1, seed=42 + i)).to(dev) for i in range(8)]
             alone = alone_leg(dev_imgs[0], W, H, params, batch_imgs=b8)
             del b8
