@@ -342,6 +342,10 @@ def main() -> int:
     ap.add_argument("--extra-seconds", type=float, default=2.0)
     ap.add_argument("--no-events", action="store_true",
                     help="skip the per-launch HIP events of the pyramid roofline")
+    ap.add_argument("--events-every", type=int, default=8,
+                    help="time the pyramid/extrema launches of every k-th job of the timed "
+                         "region with HIP events (per-launch events on every job slow the "
+                         "pipeline by ~5%%)")
     ap.add_argument("--no-alone", action="store_true",
                     help="skip the kernel-alone roofline legs (PMC sessions count only the "
                          "timed region's launches)")
@@ -408,15 +412,21 @@ def main() -> int:
 
     depth = JOB_DEPTH if B == 1 else BATCH_DEPTH
 
+    sample_events = False  # set for the timed region
+
     def run(n_steps: int) -> int:
         kp = 0
         if args.sync:
-            for _ in range(n_steps):
+            for k in range(n_steps):
+                if sample_events:
+                    ctx.set_profiling(k % args.events_every == 0)
                 kp += finish(submit())
             return kp
         q = collections.deque()
         for k in range(n_steps):
             while len(q) < depth and k + len(q) < n_steps:
+                if sample_events:
+                    ctx.set_profiling((k + len(q)) % args.events_every == 0)
                 q.append(submit())
             kp += finish(q.popleft())
         return kp
@@ -431,7 +441,8 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ctx.set_profiling(not args.no_events)
+    sample_events = not args.no_events and args.events_every > 0
+    sample_events_used = sample_events
     ctx.profile_table(reset=True)
     t0 = time.perf_counter()
     kp_total = run(args.steps)
@@ -441,6 +452,7 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    sample_events = False
     ctx.set_profiling(False)
     prof = ctx.profile_table(reset=True)
     pyr_rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
@@ -480,6 +492,8 @@ def main() -> int:
         traffic, traffic_note = load_traffic(args.traffic_json)
         roofline = roofline_obj(blur_ms, blur_bytes, blur_launches,
                                 traffic.get("pyramid") if traffic else None, traffic_note)
+        roofline["sampled_jobs"] = (f"per-launch HIP events on every {args.events_every}th job of "
+                                    "the timed region" if sample_events_used else None)
         roofline["kernel"] = ("Gaussian pyramid: k_blur (strip walk, octave 0 incl. the fused "
                               "gray/x2 initial blur) + k_blur_tile (LDS tiles, octaves >= 1) + "
                               "k_octaves_lds (LDS-resident small octaves); 16 B per pixel per "

@@ -834,7 +834,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     }
     const auto t_copy = clk::now();
 
-    if (ctx->profiling) {
+    {  // events of a job submitted with profiling on (bench.py samples jobs)
         for (const EventPair& e : s.pending) {
             float ems = 0.f;
             SIFT_HIP_TRY(hipEventElapsedTime(&ems, e.a, e.b));

@@ -27,10 +27,13 @@ from sift_hip import INPUT_F64_DEVICE, Context, SiftParams, synth_image  # noqa:
 def make_ctx(spec: str) -> Context:
     env = {} if spec == "base" else dict(kv.split("=", 1) for kv in spec.split(","))
     lib = env.pop("SIFT_HIP_LIB", None)
+    prof = env.pop("PROFILE", None) == "1"  # per-launch pyramid/extrema events on
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
-        return Context(0, lib_path=lib)
+        ctx = Context(0, lib_path=lib)
+        ctx.set_profiling(prof)
+        return ctx
     finally:
         for k, v in old.items():
             if v is None:
