@@ -28,11 +28,13 @@ def make_ctx(spec: str) -> Context:
     env = {} if spec == "base" else dict(kv.split("=", 1) for kv in spec.split(","))
     lib = env.pop("SIFT_HIP_LIB", None)
     prof = env.pop("PROFILE", None) == "1"  # per-launch pyramid/extrema events on
+    depth = int(env.pop("DEPTH", "0"))  # jobs in flight for this variant (0: --depth)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
         ctx = Context(0, lib_path=lib)
         ctx.set_profiling(prof)
+        ctx.ab_depth = depth
         return ctx
     finally:
         for k, v in old.items():
@@ -79,7 +81,8 @@ def main():
         if r % 2:
             order.reverse()
         for i in order:
-            t[i].append(run(ctxs[i], ptrs, W, H, params, a.steps, a.depth, a.batch)[0] * 1e3)
+            t[i].append(run(ctxs[i], ptrs, W, H, params, a.steps, ctxs[i].ab_depth or a.depth,
+                            a.batch)[0] * 1e3)
     for i, v in enumerate(a.variants):
         ratios = [x / y for x, y in zip(t[i], t[0])]
         print(f"{v:60s} mean {sum(t[i]) / len(t[i]):.4f} ms/img  min {min(t[i]):.4f}  "
