@@ -243,6 +243,7 @@ struct sift_ctx {
     bool serial = false;          // SIFT_SERIAL=1: every kernel on one stream (profiling)
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
+    bool job_pairs = false;       // SIFT_JOB_STREAMS=2: two streams per job beyond the first
     int desc_mode = 1;            // SIFT_DESC_MODE: k_descriptor variant (0 f64, 1 f32 math, 2 f32 hist)
     int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
@@ -961,10 +962,21 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
             s.uses = 0xAu;
         } else {
             int k = 0;
-            while (k + 1 < kSlots && (used >> k & 1u)) ++k;
-            s.sA = s.sB = s.sC = s.sD = q[k];
-            s.lanes = 1;
-            s.uses = 1u << k;
+            if (ctx->job_pairs) {  // SIFT_JOB_STREAMS=2: a free pair (pyramid, keypoints)
+                while (k + 2 < kSlots && (used >> k & 3u)) k += 2;
+            }
+            if (ctx->job_pairs && !(used >> k & 3u) && k + 1 < kSlots) {
+                s.sA = s.sB = q[k];
+                s.sC = s.sD = q[k + 1];
+                s.lanes = 1;
+                s.uses = 3u << k;
+            } else {
+                k = 0;
+                while (k + 1 < kSlots && (used >> k & 1u)) ++k;
+                s.sA = s.sB = s.sC = s.sD = q[k];
+                s.lanes = 1;
+                s.uses = 1u << k;
+            }
         }
         if (ctx->serial) {  // profiling: one stream, no overlap (kernel costs alone)
             s.sA = s.sB = s.sC = s.sD = q[0];
@@ -1071,6 +1083,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_SHARED_STREAMS")) ctx->shared_streams = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
+    if (const char* e = std::getenv("SIFT_JOB_STREAMS")) ctx->job_pairs = std::atoi(e) == 2;
     if (const char* e = std::getenv("SIFT_FUSE_INITIAL")) ctx->fuse_initial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_EXTREMA_TILES")) ctx->extrema_stream = std::atoi(e) == 0;
