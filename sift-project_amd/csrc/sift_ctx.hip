@@ -234,7 +234,15 @@ struct sift_ctx {
     // per CU; with two keypoint lanes in flight this leaves room for the
     // small octaves' blurs); measured best of 256/384/512/768/1024
     unsigned kp_wgs = 512;
-    int batch_px_log2 = 18;  // octaves of >= 2^this pixels (x images) get their own batch
+    // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
+    // rest form one final batch after the LDS octaves. A job sharing the chip
+    // (one stream, lanes = 1) uses 2^22: a 1080p job has two batches (octave
+    // 0, the rest), 5 % faster pipelined than four (2^18) and neutral for
+    // 8-image jobs (profiles/r02_ab/r02ap); a job alone on all four streams
+    // keeps 2^18, whose batches overlap the smaller octaves' pyramid (the
+    // synchronous latency rose from 0.90 to 1.25 ms with 2^22)
+    int batch_px_log2 = 22;
+    int batch_px_log2_alone = 18;
     size_t tile_max_px = (size_t)1 << 21;  // planes up to this size: LDS-tile blur
     // octaves of at most this many pixels (and within the LDS, lds_octave_fits)
     // run LDS-resident in the one-workgroup k_octaves_lds (SIFT_LDS_PX)
@@ -548,7 +556,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // whose keypoint work is too small to amortise a chain of launches, form
     // one final batch. The final batch starts no later than o_small: octaves
     // built by k_octaves_lds have no per-octave batch of their own.
-    const size_t batch_px = (size_t)1 << ctx->batch_px_log2;
+    const size_t batch_px = (size_t)1 << (s.lanes > 1 ? ctx->batch_px_log2_alone
+                                                    : ctx->batch_px_log2);
     int o_merge = g.octaves;  // first octave of the final batch
     for (int o = 0; o < g.octaves; ++o)
         if ((size_t)g.W[o] * g.H[o] * n_img < batch_px) {
@@ -1077,9 +1086,11 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
     if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::atoi(e);
     if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
-    if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) ctx->batch_px_log2 = std::atoi(e);
+    if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2"))
+        ctx->batch_px_log2 = ctx->batch_px_log2_alone = std::atoi(e);
     if (const char* e = std::getenv("SIFT_KP_LANES")) ctx->lanes = std::atoi(e) == 1 ? 1 : kLanes;
-    if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 18;
+    if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 22;
+    if (ctx->batch_px_log2_alone < 0 || ctx->batch_px_log2_alone > 40) ctx->batch_px_log2_alone = 18;
     if (const char* e = std::getenv("SIFT_SHARED_STREAMS")) ctx->shared_streams = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
