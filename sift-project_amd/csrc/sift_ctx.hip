@@ -235,12 +235,13 @@ struct sift_ctx {
     // small octaves' blurs); measured best of 256/384/512/768/1024
     unsigned kp_wgs = 512;
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
-    // rest form one final batch after the LDS octaves. A job sharing the chip
-    // (one stream, lanes = 1) uses 2^22: a 1080p job has two batches (octave
-    // 0, the rest), 5 % faster pipelined than four (2^18) and neutral for
-    // 8-image jobs (profiles/r02_ab/r02ap); a job alone on all four streams
-    // keeps 2^18, whose batches overlap the smaller octaves' pyramid (the
-    // synchronous latency rose from 0.90 to 1.25 ms with 2^22)
+    // rest form one final batch after the LDS octaves. A single-image job
+    // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
+    // batches (octave 0, the rest), 5 % faster pipelined than four (2^18).
+    // Jobs alone on all four streams and multi-image jobs keep 2^18: the
+    // batches overlap the smaller octaves' pyramid (2^22 raised the
+    // synchronous latency from 0.90 to 1.25 ms and 8-image jobs by 4 %;
+    // profiles/r02_ab/r02ap, r02as)
     int batch_px_log2 = 22;
     int batch_px_log2_alone = 18;
     size_t tile_max_px = (size_t)1 << 21;  // planes up to this size: LDS-tile blur
@@ -556,8 +557,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // whose keypoint work is too small to amortise a chain of launches, form
     // one final batch. The final batch starts no later than o_small: octaves
     // built by k_octaves_lds have no per-octave batch of their own.
-    const size_t batch_px = (size_t)1 << (s.lanes > 1 ? ctx->batch_px_log2_alone
-                                                    : ctx->batch_px_log2);
+    const size_t batch_px = (size_t)1 << ((s.lanes > 1 || n_img > 1) ? ctx->batch_px_log2_alone
+                                                                  : ctx->batch_px_log2);
     int o_merge = g.octaves;  // first octave of the final batch
     for (int o = 0; o < g.octaves; ++o)
         if ((size_t)g.W[o] * g.H[o] * n_img < batch_px) {
