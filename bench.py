@@ -73,8 +73,9 @@ def cpu_baseline(img: np.ndarray, seconds: float) -> dict:
         "cores": 1,
         "kind": "port",
         "sample": f"{runs} x full 1920x1080 synthetic image (seed 42) through oracle/sift_cpu.cpp "
-                  f"(copy-fixed-equivalent restatement, single thread, {cpu_model()}), "
-                  f"{t_total:.1f} s",
+                  f"(the oracle restatement, bit-identical output; ~3x faster than the "
+                  f"reference's own copy-fixed code on the same core, whose column-major blur "
+                  f"walk dominates it; single thread, {cpu_model()}), {t_total:.1f} s",
     }
 
 
@@ -204,6 +205,28 @@ def alone_leg(dev_img, W, H, params, n_images: int = 200, batch_imgs=None) -> di
                                 f"kernel covers the job), SIFT_SERIAL=1 context"}
     sctx.close()
     return out
+
+
+def desc_mode_leg(ptrs, W, H, params, n_steps: int, depth: int, mode: int) -> dict:
+    """The same pipelined step as the timed region, on a second context whose
+    descriptor kernel runs in SIFT_DESC_MODE=`mode` (0: every per-sample
+    operation in f64, as src/sift.cpp:641-678; 1, the default: exact f64
+    sample acceptance, f32 sample math, f64 histograms)."""
+    prev = os.environ.get("SIFT_DESC_MODE")
+    os.environ["SIFT_DESC_MODE"] = str(mode)
+    try:
+        c = Context(torch.cuda.current_device())
+    finally:
+        if prev is None:
+            del os.environ["SIFT_DESC_MODE"]
+        else:
+            os.environ["SIFT_DESC_MODE"] = prev
+    sub = lambda k: c.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params)  # noqa: E731
+    pipelined(c, sub, 4 * depth, depth)
+    kp, dt = pipelined(c, sub, n_steps, depth)
+    c.close()
+    return {"value": kp / dt, "unit": "keypoints/s", "ms_per_step": dt / n_steps * 1e3,
+            "steps": n_steps, "desc_mode": mode}
 
 
 def pipelined(ctx, submit, n_steps: int, depth: int = 0):
@@ -337,6 +360,8 @@ def main() -> int:
                          "data path on one GPU)")
     ap.add_argument("--sync", action="store_true",
                     help="one job at a time (no pipelining), for profiling / A-B")
+    ap.add_argument("--no-desc-f64", action="store_true",
+                    help="skip the all-f64 descriptor leg (value_desc_f64)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the latency / API / batch8 legs")
     ap.add_argument("--extra-seconds", type=float, default=2.0)
@@ -435,7 +460,8 @@ def main() -> int:
     kp_per_image = ctx.counts()["final_n"] // B
     if use_exchange:
         from sift_dist import RecordExchange, agree_capacity
-        exchange = RecordExchange(agree_capacity(max_rows, dev), dev, max_images=max(16, B))
+        exchange = RecordExchange(agree_capacity(max_rows, dev), dev, max_images=max(16, B),
+                                  verify_ctx=ctx)
         run(1)  # one untimed pipelined step
 
     if world > 1:
@@ -470,16 +496,23 @@ def main() -> int:
         ok, n_recv = 1, len(got)
         for j in range(B):
             i = peer * B + j
-            ref, _ = ctx.detect_device(
-                torch.from_numpy(synth_image(W, H, 1, seed=42 + i)).to(dev).data_ptr(), W, H, 1,
-                params)
+            peer_img = torch.from_numpy(synth_image(W, H, 1, seed=42 + i)).to(dev)
+            torch.cuda.synchronize()  # the library's stream does not wait on torch's
+            ref, _ = ctx.detect_device(peer_img.data_ptr(), W, H, 1, params)
+            del peer_img
             ok &= int(i in got and got[i].cpu().numpy().tobytes() == ref.tobytes())
-        chk = torch.tensor([ok, n_recv], dtype=torch.int64, device=dev)
-        dist.all_reduce(chk[:1], op=dist.ReduceOp.MIN)
-        dist.all_reduce(chk[1:], op=dist.ReduceOp.MIN)
+        bad = exchange.mismatches()
+        chk = torch.tensor([ok, n_recv, bad, exchange.checked], dtype=torch.int64, device=dev)
+        dist.all_reduce(chk[:2], op=dist.ReduceOp.MIN)
+        dist.all_reduce(chk[2:], op=dist.ReduceOp.SUM)
         exchange_check = {"records_match_peer_redetect": bool(chk[0]),
                           "min_images_received_per_rank": int(chk[1]),
-                          "images_per_step": world * B}
+                          "images_per_step": world * B,
+                          "slots_checksummed": int(chk[3]),
+                          "slot_checksum_mismatches": int(chk[2]),
+                          "note": "every step: each received slot's records summed on the device "
+                                  "against its sender's checksum (sift_hip_verify_slots); last "
+                                  "step: peer images re-detected and compared byte for byte"}
         t = torch.tensor([elapsed, float(kp_total)], dtype=torch.float64, device=dev)
         t_max = t.clone()
         dist.all_reduce(t_max[:1], op=dist.ReduceOp.MAX)
@@ -519,6 +552,11 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
+            "dtype_note": ("pyramid, DoG, extrema, refine, orientation and all histograms in f64 "
+                           "(the reference's arithmetic); the default descriptor (desc_mode 1) "
+                           "decides sample acceptance in f64 and does the per-sample math "
+                           "(rotation, magnitude, atan2, exp, trilinear weights) in f32; "
+                           "value_desc_f64 is the all-f64 descriptor (desc_mode 0)"),
             "data": "synthetic (deterministic integer-RNG generator: sinusoid + Gaussian blobs, "
                     "~w*h/52 blobs, sigma 1.5-7.5)",
             "config": {
@@ -528,6 +566,7 @@ def main() -> int:
                 "image": f"{W}x{H}x1",
                 "images_per_gpu_per_step": B,
                 "jobs_in_flight": depth,
+                "desc_mode": int(os.environ.get("SIFT_DESC_MODE", "1")),
                 "keypoints_per_image": kp_per_image,
                 "parallelism": f"image-sharded x{world}" + (
                     ", RCCL all-gather of the descriptor records straight from HBM "
@@ -547,6 +586,10 @@ def main() -> int:
             roofline["alone_batch8"] = alone["batch"]["pyramid"]
             roofline["alone_batch8"]["note"] = alone["batch"]["note"]
             extrema_roofline["alone_batch8"] = alone["batch"]["extrema"]
+        if world == 1 and not args.no_desc_f64:
+            leg = desc_mode_leg(ptrs, W, H, params, max(args.steps, 400), depth, 0)
+            out["value_desc_f64"] = leg["value"]
+            out["desc_f64_leg"] = leg
         if exchange_check is not None:
             out["exchange_check"] = exchange_check
         if world == 1 and not args.no_extra:

@@ -174,6 +174,28 @@ int sift_hip_fetch(sift_ctx* ctx, int ticket, sift_kp* out, float* desc_f32);
  * SIFT_ERR_ARG (job kept) when cap < the job's total. */
 int sift_hip_fetch_device(sift_ctx* ctx, int ticket, void* d_out, size_t cap);
 
+/* Asynchronous sift_hip_fetch_device: the device gather is enqueued on the
+ * library's stream and `stream` (a hipStream_t of the caller, optional)
+ * waits for it with an event, so the caller can hand d_out to a collective
+ * with no host synchronisation. The job is released on return; its slot is
+ * reused only once the gather has completed. With d_checksum (device
+ * memory, optional) the wrapping 64-bit sum of every 8-byte word of the
+ * records written is stored there (zeroed first), for
+ * sift_hip_verify_slots. */
+int sift_hip_fetch_device_async(sift_ctx* ctx, int ticket, void* d_out, size_t cap,
+                                void* stream, uint64_t* d_checksum);
+
+/* Exchange verification for the multi-GPU driver: n_slots slots of
+ * slot_bytes each at d_slots (device memory); slot r holds at 8-byte word
+ * count_word its record count n and at word sum_word the sender's checksum
+ * (sift_hip_fetch_device_async), with the n 168-byte records after hdr_rows
+ * header rows of 168 bytes. Every slot whose records do not sum to its
+ * checksum (or whose n exceeds cap_rows) adds 1 to *d_bad (device memory).
+ * Enqueued on `stream` (default: the context's), no host wait. */
+int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_t slot_bytes,
+                          int hdr_rows, int count_word, int sum_word, size_t cap_rows,
+                          uint64_t* d_bad, void* stream);
+
 /* submit + wait + fetch into library-allocated storage (sift_hip_free):
  * *out_kps image-major, counts[b] per image. */
 int sift_hip_detect_batch(sift_ctx* ctx, const void* const* images, int n_images,

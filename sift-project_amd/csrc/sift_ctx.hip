@@ -220,6 +220,10 @@ struct Slot {
     Pinned<float> h_df32;
     Pinned<GatherItem> h_gather;  // fetch_device: (record index, size) per final record
     DevBuf<GatherItem> d_gather;
+    // an asynchronous device fetch still reading this slot's records:
+    // completed before the slot is reused (sift_hip_fetch_device_async)
+    hipEvent_t gather_ev = nullptr;
+    bool gather_pending = false;
     sift_counts counts{};
     clk::time_point t_submit;
     double t_host[5] = {0, 0, 0, 0, 0};
@@ -937,6 +941,10 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     }
     if (!sp) return SIFT_ERR_STATE;  // SIFT_MAX_INFLIGHT jobs already in flight
     Slot& s = *sp;
+    if (s.gather_pending) {  // an async device fetch may still read its records
+        SIFT_HIP_TRY(hipEventSynchronize(s.gather_ev));
+        s.gather_pending = false;
+    }
     int st = host_plan(p, w, h, c, &s.g, &s.taps_init, s.taps, &s.dp);
     if (st != SIFT_OK) return st;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
@@ -1024,31 +1032,41 @@ void gather(Slot& s, sift_kp* out, float* df) {
     s.t_host[4] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
 }
 
-// final records of a finalised job into device memory, ordered on the
-// slot's keypoint stream and completed before return
-int gather_device(Slot& s, sift_kp* d_out) {
+// final records of a finalised job into device memory, enqueued on the
+// slot's keypoint stream; `consumer` (optional) is ordered after the gather
+// by an event, so the caller's stream can use d_out with no host wait. The
+// slot's buffers stay in use until gather_ev, which a reuse of the slot waits
+// for (submit_impl).
+int gather_device(Slot& s, sift_kp* d_out, hipStream_t consumer, unsigned long long* checksum) {
     const size_t n = s.n_final;
-    if (n == 0) return SIFT_OK;
     int st;
-    if ((st = s.h_gather.ensure(n)) != SIFT_OK || (st = s.d_gather.ensure(n)) != SIFT_OK)
-        return st;
-    for (size_t i = 0; i < n; ++i) {
-        const unsigned pos = s.keep[i];  // host position of the record
-        int L;
-        size_t j;
-        if (s.exported) {
-            L = (int)(pos / s.exp_lane);
-            j = pos - (size_t)L * s.exp_lane;
-        } else {
-            L = pos < s.n_lane[0] ? 0 : 1;
-            j = pos - (L ? s.n_lane[0] : 0);
+    if (checksum) SIFT_HIP_TRY(hipMemsetAsync(checksum, 0, sizeof *checksum, s.sC));
+    if (n > 0) {
+        if ((st = s.h_gather.ensure(n)) != SIFT_OK || (st = s.d_gather.ensure(n)) != SIFT_OK)
+            return st;
+        for (size_t i = 0; i < n; ++i) {
+            const unsigned pos = s.keep[i];  // host position of the record
+            int L;
+            size_t j;
+            if (s.exported) {
+                L = (int)(pos / s.exp_lane);
+                j = pos - (size_t)L * s.exp_lane;
+            } else {
+                L = pos < s.n_lane[0] ? 0 : 1;
+                j = pos - (L ? s.n_lane[0] : 0);
+            }
+            s.h_gather.p[i] = GatherItem{s.rec_src[pos].size, (unsigned)(L * s.cap_ori + j), 0};
         }
-        s.h_gather.p[i] = GatherItem{s.rec_src[pos].size, (unsigned)(L * s.cap_ori + j), 0};
+        SIFT_HIP_TRY(hipMemcpyAsync(s.d_gather.p, s.h_gather.p, n * sizeof(GatherItem),
+                                    hipMemcpyHostToDevice, s.sC));
+        SIFT_HIP_TRY(launch_gather_records(s.ori.p, s.d_gather.p, (unsigned)n, d_out, checksum,
+                                           s.sC));
     }
-    SIFT_HIP_TRY(hipMemcpyAsync(s.d_gather.p, s.h_gather.p, n * sizeof(GatherItem),
-                                hipMemcpyHostToDevice, s.sC));
-    SIFT_HIP_TRY(launch_gather_records(s.ori.p, s.d_gather.p, (unsigned)n, d_out, s.sC));
-    SIFT_HIP_TRY(hipStreamSynchronize(s.sC));
+    if (!s.gather_ev)
+        SIFT_HIP_TRY(hipEventCreateWithFlags(&s.gather_ev, hipEventDisableTiming));
+    SIFT_HIP_TRY(hipEventRecord(s.gather_ev, s.sC));
+    s.gather_pending = true;
+    if (consumer && consumer != s.sC) SIFT_HIP_TRY(hipStreamWaitEvent(consumer, s.gather_ev, 0));
     return SIFT_OK;
 }
 
@@ -1164,6 +1182,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
         s.h_df32.release();
         s.h_gather.release();
         s.d_gather.release();
+        if (s.gather_ev) (void)hipEventDestroy(s.gather_ev);
         for (hipEvent_t e : s.chain_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : s.sync_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : s.ev_pool) (void)hipEventDestroy(e);
@@ -1219,10 +1238,47 @@ int sift_hip_fetch_device(sift_ctx* ctx, int ticket, void* d_out, size_t cap) {
     if (st != SIFT_OK) return st;
     if (cap < s->n_final) return SIFT_ERR_ARG;  // the job stays fetchable
     (void)hipSetDevice(ctx->device);
-    st = gather_device(*s, static_cast<sift_kp*>(d_out));
+    st = gather_device(*s, static_cast<sift_kp*>(d_out), nullptr, nullptr);
+    if (st == SIFT_OK) SIFT_HIP_TRY(hipEventSynchronize(s->gather_ev));
+    s->gather_pending = false;
     s->state = kFree;
     s->ticket = -1;
     return st;
+}
+
+int sift_hip_fetch_device_async(sift_ctx* ctx, int ticket, void* d_out, size_t cap,
+                                void* stream, uint64_t* d_checksum) {
+    if (!ctx || (!d_out && cap)) return SIFT_ERR_ARG;
+    Slot* s = slot_of(ctx, ticket);
+    if (!s) return SIFT_ERR_STATE;
+    int st = wait_impl(ctx, *s);
+    if (st != SIFT_OK) return st;
+    if (cap < s->n_final) return SIFT_ERR_ARG;  // the job stays fetchable
+    (void)hipSetDevice(ctx->device);
+    st = gather_device(*s, static_cast<sift_kp*>(d_out), static_cast<hipStream_t>(stream),
+                       reinterpret_cast<unsigned long long*>(d_checksum));
+    if (st != SIFT_OK) {  // nothing usable was enqueued past this point: drain
+        abandon(ctx, *s);
+        return st;
+    }
+    s->state = kFree;
+    s->ticket = -1;
+    return SIFT_OK;
+}
+
+int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_t slot_bytes,
+                          int hdr_rows, int count_word, int sum_word, size_t cap_rows,
+                          uint64_t* d_bad, void* stream) {
+    if (!ctx || !d_bad || (n_slots > 0 && !d_slots) || n_slots < 0 || hdr_rows < 0 ||
+        count_word < 0 || sum_word < 0 || slot_bytes % 8 ||
+        (size_t)(count_word + 1) * 8 > slot_bytes || (size_t)(sum_word + 1) * 8 > slot_bytes ||
+        ((size_t)hdr_rows + cap_rows) * sizeof(sift_kp) > slot_bytes)
+        return SIFT_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    SIFT_HIP_TRY(launch_verify_slots(d_slots, n_slots, slot_bytes, hdr_rows, count_word, sum_word,
+                                     cap_rows, reinterpret_cast<unsigned long long*>(d_bad), st));
+    return SIFT_OK;
 }
 
 int sift_hip_detect_batch(sift_ctx* ctx, const void* const* images, int n_images,

@@ -7,7 +7,6 @@
 #include <cstdint>
 #include <cstring>
 #include <numeric>
-#include <thread>
 #include <vector>
 
 namespace sift_amd {
@@ -232,41 +231,6 @@ size_t host_finalize(const sift_params* p, sift_kp* recs, const RecSide* side, u
     ws->all.resize(n);
     host_sort_run(recs, side, 0, n, ws->all.data(), ws);
     return host_merge_unique(ws->all.data(), {0u, n}, keep, per_img, ws);
-}
-
-namespace {
-
-bool pack_range(const double* src, size_t n, uint8_t* dst) {
-    bool ok = true;
-    for (size_t i = 0; i < n; ++i) {
-        const double v = src[i];
-        const uint8_t u = (v >= 0.0 && v <= 255.0) ? (uint8_t)v : 0;
-        const double back = (double)u;
-        ok &= std::memcmp(&back, &v, sizeof v) == 0;  // bit-identical round trip
-        dst[i] = u;
-    }
-    return ok;
-}
-
-}  // namespace
-
-bool host_pack_u8(const double* src, size_t n, uint8_t* dst) {
-    const size_t kChunk = (size_t)1 << 19;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned nt = (unsigned)std::min<size_t>({(size_t)8, (size_t)hw, (n + kChunk - 1) / kChunk});
-    if (nt <= 1) return pack_range(src, n, dst);
-    std::vector<std::thread> th;
-    std::vector<char> ok(nt, 1);
-    const size_t per = (n + nt - 1) / nt;
-    for (unsigned t = 1; t < nt; ++t) {
-        const size_t b = std::min(n, t * per), e = std::min(n, b + per);
-        th.emplace_back([=, &ok] { ok[t] = pack_range(src + b, e - b, dst + b); });
-    }
-    ok[0] = pack_range(src, std::min(n, per), dst);
-    for (auto& t : th) t.join();
-    for (char c : ok)
-        if (!c) return false;
-    return true;
 }
 
 }  // namespace sift_amd

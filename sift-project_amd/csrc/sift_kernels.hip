@@ -1374,14 +1374,16 @@ __device__ void describe(DescLdsT<MODE>& S, const PyrTable* __restrict__ pt, con
             scol = lo_r + (t - ex_r);
             return t < total;
         };
+        // The four gradient loads are issued unconditionally (lanes past the
+        // end read pixel (1, 1)): loads under a branch leave the compiler's
+        // wait-count bookkeeping unable to count them, and it then waits for
+        // the prefetched sample before processing the current one
         auto fetch = [&](bool ok, int srow, int scol, double* v) {
-            if (ok) {
-                const size_t r0 = (size_t)(srow + y) * W + scol + x;
-                v[0] = img[r0 + 1];
-                v[1] = img[r0 - 1];
-                v[2] = img[r0 - W];
-                v[3] = img[r0 + W];
-            }
+            const size_t r0 = ok ? (size_t)(srow + y) * W + scol + x : (size_t)W + 1;
+            v[0] = img[r0 + 1];
+            v[1] = img[r0 - 1];
+            v[2] = img[r0 - W];
+            v[3] = img[r0 + W];
         };
         // kAhead samples ahead: the next samples' gradient loads are in
         // flight while the current one is processed
@@ -1617,15 +1619,18 @@ __global__ __launch_bounds__(256, 4) void k_orient(
                 ++j;
             }
         };
+        // unconditional loads (samples outside the image read pixel (1, 1)),
+        // so the next sample's loads stay in flight while this one is
+        // processed (see describe's fetch)
         auto fetch = [&](int s, int i, int j, double* v) -> bool {
-            if (s >= nsamp || x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H)
-                return false;
-            const size_t r0 = (size_t)(y + j) * W + x + i;
+            const bool ok =
+                !(s >= nsamp || x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H);
+            const size_t r0 = ok ? (size_t)(y + j) * W + x + i : (size_t)W + 1;
             v[0] = img[r0 + 1];
             v[1] = img[r0 - 1];
             v[2] = img[r0 - W];
             v[3] = img[r0 + W];
-            return true;
+            return ok;
         };
         double cv[4], nv[4];
         bool cok = fetch(tid, ci_, cj_, cv);
@@ -1988,23 +1993,79 @@ hipError_t launch_u8_to_f64(const uint8_t* in, double* out, size_t n, hipStream_
 
 // Final records of a job gathered on the device: out[i] = recs[src[i]]
 // with the host's glibc-exact size (sift.cpp:427-429) patched in. One
-// 64-lane wave per record, 168 B = 21 doubles.
+// 64-lane wave per record, 168 B = 21 doubles. With `checksum`, the wrapping
+// 64-bit sum of every word written is added to *checksum (one atomic per
+// workgroup), so a receiver of the records can verify them.
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_gather_records(const sift_kp* __restrict__ recs,
                                                         const GatherItem* __restrict__ items,
-                                                        unsigned n, sift_kp* __restrict__ out) {
+                                                        unsigned n, sift_kp* __restrict__ out,
+                                                        unsigned long long* __restrict__ checksum) {
+    __shared__ unsigned long long part[4];
     const unsigned i = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (i >= n) return;
-    const GatherItem it = items[i];
-    const double* src = reinterpret_cast<const double*>(recs + it.src);
-    double* dst = reinterpret_cast<double*>(out + i);
-    if (lane < 21) dst[lane] = (lane == 3) ? it.size : src[lane];  // size @ byte 24
+    unsigned long long word = 0;
+    if (i < n) {
+        const GatherItem it = items[i];
+        const double* src = reinterpret_cast<const double*>(recs + it.src);
+        double* dst = reinterpret_cast<double*>(out + i);
+        if (lane < 21) {
+            const double v = (lane == 3) ? it.size : src[lane];  // size @ byte 24
+            dst[lane] = v;
+            word = (unsigned long long)__double_as_longlong(v);
+        }
+    }
+    if (!checksum) return;
+    word = wave_sum_u64(word);
+    if (lane == 0) part[threadIdx.x >> 6] = word;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(checksum, part[0] + part[1] + part[2] + part[3]);
 }
 
 hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, unsigned n,
-                                 sift_kp* out, hipStream_t s) {
+                                 sift_kp* out, unsigned long long* checksum, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gather_records, dim3((n + 3) / 4), dim3(256), 0, s, recs, items, n, out);
+    hipLaunchKernelGGL(k_gather_records, dim3((n + 3) / 4), dim3(256), 0, s, recs, items, n, out,
+                       checksum);
+    return hipGetLastError();
+}
+
+// Exchange verification (sift_hip_verify_slots): slot r of `slots` holds,
+// from word `count_word`, the number of 168-B records after `hdr_rows`
+// header rows, and at word `sum_word` the sender's checksum of them
+// (k_gather_records). One workgroup per slot; a mismatch increments *bad.
+__global__ __launch_bounds__(256) void k_verify_slots(const unsigned long long* __restrict__ slots,
+                                                      size_t slot_words, int hdr_rows,
+                                                      int count_word, int sum_word,
+                                                      size_t cap_rows,
+                                                      unsigned long long* __restrict__ bad) {
+    __shared__ unsigned long long part[4];
+    const unsigned long long* sl = slots + (size_t)blockIdx.x * slot_words;
+    const unsigned long long n = sl[count_word];
+    const size_t words = (size_t)(n < cap_rows ? n : cap_rows) * 21;
+    const unsigned long long* rec = sl + (size_t)hdr_rows * 21;
+    unsigned long long v = 0;
+    for (size_t k = threadIdx.x; k < words; k += 256) v += rec[k];
+    v = wave_sum_u64(v);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        (n > cap_rows || part[0] + part[1] + part[2] + part[3] != sl[sum_word]))
+        atomicAdd(bad, 1ull);
+}
+
+hipError_t launch_verify_slots(const void* slots, int n_slots, size_t slot_bytes, int hdr_rows,
+                               int count_word, int sum_word, size_t cap_rows,
+                               unsigned long long* bad, hipStream_t s) {
+    if (n_slots <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_verify_slots, dim3(n_slots), dim3(256), 0, s,
+                       static_cast<const unsigned long long*>(slots), slot_bytes / 8, hdr_rows,
+                       count_word, sum_word, cap_rows, bad);
     return hipGetLastError();
 }
 

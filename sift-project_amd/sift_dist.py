@@ -17,6 +17,7 @@ from __future__ import annotations
 import math
 from typing import Dict, List, Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -102,15 +103,25 @@ class RecordExchange:
     from the records in HBM), so the payload never crosses PCIe.
     """
 
-    def __init__(self, cap_rows: int, device: torch.device, group=None, max_images: int = 16):
+    def __init__(self, cap_rows: int, device: torch.device, group=None, max_images: int = 16,
+                 verify_ctx=None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.cap = int(cap_rows)
         self.device = device
         self.cuda = device.type == "cuda"
         self.max_images = int(max_images)
-        self.hdr_words = 2 + 2 * self.max_images
+        # header words: image count, record count, (image id, count) per
+        # image, then the sender's checksum of its records (the wrapping
+        # 64-bit sum of their 8-byte words): every received slot of every
+        # step is checked against it (on the device with `verify_ctx`, a
+        # sift_hip.Context, under RCCL; on the host under gloo)
+        self.sum_word = 2 + 2 * self.max_images
+        self.hdr_words = self.sum_word + 1
         self.hdr_rows = math.ceil(self.hdr_words * 8 / RECORD_BYTES)
+        self.verify_ctx = verify_ctx
+        self.bad = torch.zeros(1, dtype=torch.int64, device=device)
+        self.checked = 0
         rows = self.cap + self.hdr_rows
         pin = self.cuda
         self.host = [torch.zeros((rows, RECORD_BYTES), dtype=torch.uint8, pin_memory=pin)
@@ -126,9 +137,24 @@ class RecordExchange:
 
     def _wait_slot(self, s: int) -> None:
         if self.done[s] is not None:
-            self.done[s].synchronize() if self.cuda else self.work[s].wait()
+            if self.cuda:
+                self.done[s].synchronize()
+            else:
+                self.work[s].wait()
+                self._verify_host(s)
             self.done[s] = None
             self.work[s] = None
+
+    def _verify_host(self, s: int) -> None:
+        rows = self.cap + self.hdr_rows
+        g = self.gathered[s].view(self.world, rows * RECORD_BYTES).numpy()
+        for r in range(self.world):
+            w = g[r].view("<u8")
+            n = int(w[1])
+            recs = w[self.hdr_rows * RECORD_BYTES // 8:][: min(n, self.cap) * RECORD_BYTES // 8]
+            if n > self.cap or int(recs.sum(dtype="<u8")) != int(w[self.sum_word]):
+                self.bad += 1
+        self.checked += self.world
 
     def _next_slot(self) -> int:
         s = self.step & 1
@@ -137,9 +163,10 @@ class RecordExchange:
         return s
 
     def _header(self, counts: Sequence[int], image_ids: Sequence[int]) -> torch.Tensor:
+        """The header words before the checksum (host-built)."""
         if len(counts) > self.max_images:
             raise ValueError(f"{len(counts)} images per step > max_images={self.max_images}")
-        hdr = torch.zeros(self.hdr_rows * RECORD_BYTES // 8, dtype=torch.int64)
+        hdr = torch.zeros(self.sum_word, dtype=torch.int64)
         hdr[0] = len(counts)
         hdr[1] = sum(int(c) for c in counts)
         for j, (c, i) in enumerate(zip(counts, image_ids)):
@@ -158,6 +185,13 @@ class RecordExchange:
                 self.work[s] = dist.all_gather_into_tensor(self.gathered[s], self.dev[s],
                                                            group=self.group, async_op=True)
                 self.work[s].wait()  # orders the side stream after the collective
+                if self.verify_ctx is not None:
+                    rows = self.cap + self.hdr_rows
+                    self.verify_ctx.verify_slots(
+                        self.gathered[s].data_ptr(), self.world, rows * RECORD_BYTES,
+                        self.hdr_rows, 1, self.sum_word, self.cap, self.bad.data_ptr(),
+                        self.stream.cuda_stream)
+                    self.checked += self.world
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
                 self.done[s] = ev
@@ -179,6 +213,9 @@ class RecordExchange:
             n = min(int(t.shape[0]), self.cap + self.hdr_rows - off)
             h[off: off + n] = t[:n]
             off += n
+        words = h[self.hdr_rows: off].numpy().view("<u8")
+        h.view(-1)[self.sum_word * 8:(self.sum_word + 1) * 8] = torch.from_numpy(
+            np.array([words.sum(dtype="<u8")], dtype="<u8").view(np.uint8))
         self._launch(s, off * RECORD_BYTES)
         return s
 
@@ -190,16 +227,31 @@ class RecordExchange:
         n_rows = sum(counts)
         s = self._next_slot()
         base = self.dev[s][self.hdr_rows:]
+        chk = self.dev[s].view(-1)[self.sum_word * 8:(self.sum_word + 1) * 8]
         if n_rows <= self.cap:
-            sift_ctx.fetch_device(ticket, base.data_ptr(), self.cap)
+            # gathered on the library's stream; the side stream waits on it
+            # with an event (no host synchronisation), and the library adds
+            # the records' word sum into the slot's checksum word
+            sift_ctx.fetch_device_async(ticket, base.data_ptr(), self.cap,
+                                        self.stream.cuda_stream, chk.data_ptr())
         else:  # overflow: truncated and flagged, as push does
+            cur = torch.cuda.current_stream(self.device)
             tmp = torch.empty((n_rows, RECORD_BYTES), dtype=torch.uint8, device=self.device)
-            sift_ctx.fetch_device(ticket, tmp.data_ptr(), n_rows)
+            sift_ctx.fetch_device_async(ticket, tmp.data_ptr(), n_rows, cur.cuda_stream)
             base.copy_(tmp[: self.cap])
+            w = base.view(-1).view(torch.int64)  # torch sums int64 with wrap-around
+            chk.view(torch.int64).copy_(w.sum().view(1))
         hdr = self._header(counts, image_ids)
         self.host[s].view(-1)[: hdr.numel()] = hdr
         self._launch(s, hdr.numel())
         return s
+
+    def mismatches(self) -> int:
+        """Slots (one per rank per completed step) whose records did not sum
+        to their sender's checksum; call flush first."""
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+        return int(self.bad.item())
 
     def flush(self) -> None:
         """Wait for every exchange in flight."""

@@ -71,6 +71,8 @@ EXPORTS = (
     "sift_hip_wait",
     "sift_hip_fetch",
     "sift_hip_fetch_device",
+    "sift_hip_fetch_device_async",
+    "sift_hip_verify_slots",
     "sift_hip_detect_batch",
     "sift_hip_match",
     "sift_hip_match_device",
@@ -188,6 +190,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sift_hip_wait.argtypes = [vp, i, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     lib.sift_hip_fetch.argtypes = [vp, i, vp, vp]
     lib.sift_hip_fetch_device.argtypes = [vp, i, vp, sz]
+    lib.sift_hip_fetch_device_async.argtypes = [vp, i, vp, sz, vp, vp]
+    lib.sift_hip_verify_slots.argtypes = [vp, vp, i, sz, i, i, i, sz, vp, vp]
     lib.sift_hip_detect_batch.argtypes = [vp, ctypes.POINTER(vp), i, i, i, i, i,
                                           ctypes.POINTER(CParams), ctypes.POINTER(vp),
                                           ctypes.POINTER(sz), ctypes.POINTER(vp)]
@@ -276,8 +280,20 @@ class Context:
         alive until wait(); returns the ticket."""
         n = len(images)
         ptrs = (ctypes.c_void_p * n)()
+        host = kind in (INPUT_F64_HOST, INPUT_U8_HOST)
+        want = np.float64 if kind == INPUT_F64_HOST else np.uint8
         for b, im in enumerate(images):
-            ptrs[b] = im if isinstance(im, int) else im.ctypes.data
+            if host:
+                # the library copies exactly w*h*c elements of this dtype
+                if not isinstance(im, np.ndarray) or im.dtype != want or \
+                        not im.flags["C_CONTIGUOUS"] or im.size != w * h * c:
+                    raise ValueError(f"image {b}: expected a C-contiguous {np.dtype(want).name} "
+                                     f"array of {w}x{h}x{c} elements")
+                ptrs[b] = im.ctypes.data
+            else:
+                if not isinstance(im, int):
+                    raise ValueError(f"image {b}: device inputs are integer pointers")
+                ptrs[b] = im
         p = (params or SiftParams()).to_c()
         t = ctypes.c_int()
         _check(self.lib.sift_hip_submit(self._ctx, ptrs, n, kind, w, h, c, ctypes.byref(p),
@@ -320,6 +336,29 @@ class Context:
         del self._jobs[ticket]
         return counts
 
+    def fetch_device_async(self, ticket: int, dev_ptr: int, cap: int, stream: int = 0,
+                           checksum_ptr: int = 0):
+        """fetch_device without a host wait: the gather is enqueued on the
+        library's stream and `stream` (hipStream_t handle, e.g. a torch
+        stream's cuda_stream) is ordered after it; optionally the records'
+        64-bit word sum goes to device memory at checksum_ptr. Releases the
+        job; returns per-image counts."""
+        counts = self.wait(ticket)
+        _check(self.lib.sift_hip_fetch_device_async(
+            self._ctx, ticket, ctypes.c_void_p(dev_ptr), cap, ctypes.c_void_p(stream or None),
+            ctypes.c_void_p(checksum_ptr or None)))
+        del self._jobs[ticket]
+        return counts
+
+    def verify_slots(self, slots_ptr: int, n_slots: int, slot_bytes: int, hdr_rows: int,
+                     count_word: int, sum_word: int, cap_rows: int, bad_ptr: int,
+                     stream: int = 0) -> None:
+        """Enqueue the exchange check of n_slots record slots (see
+        include/sift_hip.h sift_hip_verify_slots)."""
+        _check(self.lib.sift_hip_verify_slots(
+            self._ctx, ctypes.c_void_p(slots_ptr), n_slots, slot_bytes, hdr_rows, count_word,
+            sum_word, cap_rows, ctypes.c_void_p(bad_ptr), ctypes.c_void_p(stream or None)))
+
     def detect(self, img: np.ndarray, params: SiftParams | None = None, desc_f32: bool = False):
         """detect_keypoints_and_descriptors on a host image (H,W[,C] float64)."""
         a, w, h, c = _as_hwc(img)
@@ -348,9 +387,14 @@ class Context:
         pointers with kind=INPUT_*_DEVICE and shape=(w, h, c)); lists of
         per-image results."""
         if kind is None:
-            arrs = [_as_hwc(im)[0] for im in images]
-            _, w, h, c = _as_hwc(arrs[0])
-            return self.fetch(self.submit(arrs, INPUT_F64_HOST, w, h, c, params, desc_f32))
+            shaped = [_as_hwc(im) for im in images]
+            _, w, h, c = shaped[0]
+            for b, (_, wb, hb, cb) in enumerate(shaped):
+                if (wb, hb, cb) != (w, h, c):
+                    raise ValueError(f"image {b} is {wb}x{hb}x{cb}, image 0 is {w}x{h}x{c}: "
+                                     "a job's images share one shape")
+            return self.fetch(self.submit([a for a, *_ in shaped], INPUT_F64_HOST, w, h, c,
+                                          params, desc_f32))
         w, h, c = shape
         return self.fetch(self.submit([int(x) for x in images], kind, w, h, c, params, desc_f32))
 

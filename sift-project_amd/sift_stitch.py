@@ -180,22 +180,34 @@ def compose(graph: StitchGraph, pairs, n_images: int):
     return Hs
 
 
-def canvas_for(images, Hs, max_side: int = 8192):
-    """Translation + size of the canvas holding every warped image corner
-    (clipped to max_side per axis around the centre image)."""
-    pts = []
-    for k, H in Hs.items():
+def canvas_for(images, Hs, max_side: int = 8192, center=None):
+    """Translation + size of the canvas holding every warped image corner,
+    clipped to max_side per axis around the centre image's projected box
+    (compose() inserts the centre first). Images with a corner behind the
+    camera are left out; if that leaves none, the canvas is the centre
+    image's own box."""
+    if center is None:
+        center = next(iter(Hs))
+
+    def corners(k):
         h, w = images[k].shape[:2]
         c = np.array([[0, 0, 1], [w - 1, 0, 1], [0, h - 1, 1], [w - 1, h - 1, 1]], float).T
-        p = H @ c
-        if np.any(p[2] <= 0):
-            continue
-        pts.append((p[:2] / p[2]).T)
+        p = Hs[k] @ c
+        return None if np.any(p[2] <= 0) else (p[:2] / p[2]).T
+
+    pts = [q for q in (corners(k) for k in Hs) if q is not None]
+    cpts = corners(center)
+    if cpts is None:  # centre rotated/projected behind the camera: its raw box
+        h, w = images[center].shape[:2]
+        cpts = np.array([[0.0, 0.0], [w - 1.0, h - 1.0]])
+    if not pts:
+        pts = [cpts]
     pts = np.concatenate(pts)
     lo = np.floor(pts.min(axis=0))
     hi = np.ceil(pts.max(axis=0))
-    lo = np.maximum(lo, -max_side / 2)
-    hi = np.minimum(hi, max_side / 2)
+    mid = 0.5 * (cpts.min(axis=0) + cpts.max(axis=0))
+    lo = np.maximum(lo, np.floor(mid - max_side / 2))
+    hi = np.minimum(hi, np.floor(mid - max_side / 2) + max_side - 1)
     T = np.array([[1.0, 0.0, -lo[0]], [0.0, 1.0, -lo[1]], [0.0, 0.0, 1.0]])
     return T, int(hi[0] - lo[0]) + 1, int(hi[1] - lo[1]) + 1
 

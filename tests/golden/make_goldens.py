@@ -230,6 +230,18 @@ def make_case(name, spec, tmp, params=None, photo=None):
         out["final"] = np.frombuffer(final[idx].tobytes(), dtype=np.uint8)
         out["desc_f32"] = df[idx]
         meta["extrema_sha256"] = sha(ext.astype("<i4").tobytes())
+        # every keypoint's descriptor bytes and orientation (the records'
+        # remaining fields are pinned by coords_sha256), plus the normalised
+        # descriptor floats of a 4096-keypoint stratified sample: one random
+        # keypoint from each of 4096 equal slices of the sorted list
+        out["desc_u8_all"] = np.ascontiguousarray(final["desc"])
+        out["pori_all"] = np.ascontiguousarray(final["pori"], dtype="<f8")
+        n = len(final)
+        ns = min(4096, n)
+        edges = (np.arange(ns + 1) * n) // ns
+        sidx = edges[:-1] + (rng.random(ns) * (edges[1:] - edges[:-1])).astype(np.int64)
+        out["strat_idx"] = sidx
+        out["strat_desc_f32"] = df[sidx]
     out["meta_json"] = np.array(json.dumps(meta, sort_keys=True))
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
     print(f"{name}: octaves={meta['octaves']} extrema={meta['extrema']} "

@@ -30,6 +30,23 @@ class Golden:
         self.sample_idx = z["sample_idx"] if "sample_idx" in z else None
         self._input_u8 = z["input_u8"] if "input_u8" in z else None
 
+    def _array(self, key):
+        z = np.load(self.path, allow_pickle=False)
+        return z[key] if key in z.files else None
+
+    def full_desc_u8(self):
+        """Big goldens: every final keypoint's u8 descriptor [n, 128]."""
+        return self._array("desc_u8_all")
+
+    def full_pori(self):
+        """Big goldens: every final keypoint's orientation (f64)."""
+        return self._array("pori_all")
+
+    def strat_sample(self):
+        """Big goldens: (indices, normalised descriptor floats) of a
+        4096-keypoint stratified sample, or (None, None)."""
+        return self._array("strat_idx"), self._array("strat_desc_f32")
+
     @property
     def kind(self) -> str:
         return self.meta["kind"]

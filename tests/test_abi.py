@@ -69,3 +69,49 @@ def test_kernels_are_gfx950_code_objects():
     blob = open(LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
     assert b"k_blur" in blob and b"k_orient" in blob and b"k_descriptor" in blob
+
+
+def test_submit_rejects_host_arrays_that_do_not_match_the_shape():
+    """The library copies exactly w*h*c elements of the kind's dtype from
+    each host pointer: a smaller array, another dtype or a non-contiguous
+    view must be refused before the C call (no host out-of-bounds read)."""
+    import numpy as np
+
+    from sift_hip import INPUT_F64_HOST, INPUT_U8_HOST, Context
+
+    ctx = object.__new__(Context)  # validation happens before any library call
+    ok = np.zeros((10, 20))
+    for imgs, kind in (([np.zeros((10, 10))], INPUT_F64_HOST),
+                       ([ok, np.zeros((5, 20))], INPUT_F64_HOST),
+                       ([ok.astype(np.float32)], INPUT_F64_HOST),
+                       ([ok], INPUT_U8_HOST),
+                       ([np.zeros((10, 40))[:, ::2]], INPUT_F64_HOST),
+                       ([12345], INPUT_F64_HOST)):
+        with pytest.raises(ValueError):
+            Context.submit(ctx, imgs, kind, 20, 10, 1)
+    with pytest.raises(ValueError, match="share one shape"):
+        Context.detect_batch(ctx, [ok, np.zeros((11, 20))])
+
+
+def test_host_u8_packing_pass():
+    """The front end's host pass (csrc/host_pack.cpp, pooled AVX2): an Image
+    buffer goes up as bytes only if EVERY value survives the u8 round trip
+    bit for bit; one fraction, negative, -0.0, NaN or value > 255 anywhere
+    (vector body or scalar tail, any chunk) sends the doubles instead."""
+    import numpy as np
+
+    lib = load_library()
+    f = lib._ZN8sift_amd12host_pack_u8EPKdmPh  # sift_amd::host_pack_u8 (sift_host.h)
+    f.restype = ctypes.c_bool
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    rng = np.random.default_rng(3)
+    for n in (7, 4096 + 13, (1 << 17) * 3 + 5):
+        img = rng.integers(0, 256, size=n).astype(np.float64)
+        out = np.empty(n, np.uint8)
+        assert f(img.ctypes.data, n, out.ctypes.data)
+        assert np.array_equal(out, img.astype(np.uint8))
+        for bad in (0.5, -1.0, -0.0, np.nan, 256.0, 1e12, np.inf):
+            for pos in (0, n // 2, n - 1):
+                b = img.copy()
+                b[pos] = bad
+                assert not f(b.ctypes.data, n, out.ctypes.data), (n, bad, pos)

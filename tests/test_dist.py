@@ -89,7 +89,13 @@ def _exchange_worker(rank, world, port, out_q):
                 got.append({k: v.numpy().tobytes() for k, v in ex.result(s).items()})
             except RuntimeError:
                 got.append(None)
-        out_q.put((rank, cap, got))
+        # per-step checksums: the two overflowing slots of the last step are
+        # flagged; then a corrupted record byte in a received slot is caught
+        checks = [ex.checked, ex.mismatches()]
+        ex.gathered[1][ex.hdr_rows + 1, 17] ^= 1  # step 1's slot, rank 0's records
+        ex._verify_host(1)
+        checks.append(ex.mismatches())
+        out_q.put((rank, cap, got, checks))
     finally:
         dist.destroy_process_group()
 
@@ -107,8 +113,9 @@ def test_record_exchange_gloo():
         p.start()
     res = {}
     for _ in range(world):
-        r, cap, got = q.get(timeout=120)
+        r, cap, got, checks = q.get(timeout=120)
         res[r] = (cap, got)
+        assert checks == [3 * world, world, world + 1], checks
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -207,7 +207,7 @@ def test_gpu_batch_record_exchange_world1(gpu_ctx):
         got = allgather_records([b.to(dev) for b in bufs], ids, 4)
         for i in ids:
             assert got[i].cpu().numpy().tobytes() == kps[i].tobytes()
-        ex = RecordExchange(4096, dev)
+        ex = RecordExchange(4096, dev, verify_ctx=gpu_ctx)
         s = ex.push(bufs, ids)
         ex.flush()
         res = ex.result(s)
@@ -223,6 +223,8 @@ def test_gpu_batch_record_exchange_world1(gpu_ctx):
             res = ex.result(s)
             for i in ids:
                 assert res[i].cpu().numpy().tobytes() == kps[i].tobytes(), (step, i)
+        # every received slot of every step matched its sender's checksum
+        assert ex.checked == 4 and ex.mismatches() == 0
         # too small a destination keeps the job; then it can still be fetched
         t = gpu_ctx.submit(imgs[:1], INPUT_F64_HOST, 480, 360, 1)
         small = torch.empty((1, RECORD_BYTES), dtype=torch.uint8, device=dev)
@@ -232,3 +234,46 @@ def test_gpu_batch_record_exchange_world1(gpu_ctx):
         assert k[0].tobytes() == kps[0].tobytes()
     finally:
         dist.destroy_process_group()
+
+
+def test_gpu_fetch_device_bulk_and_exported_paths():
+    """sift_hip_fetch_device's two index paths. The first job of a
+    fresh context has export buffers for 8192 records per lane, so a dense
+    image (> 16k records) falls back to one bulk download; the next job runs
+    on the grown export buffers. Both device fetches (sync and async with a
+    checksum), on two-image jobs with both keypoint lanes, give the bytes of
+    the host fetch."""
+    import torch
+
+    from sift_hip import INPUT_F64_HOST
+
+    dev = torch.device("cuda", 0)
+    imgs = [synth_image(1600, 1200, 1, nblobs=200000, smax=2.0, seed=91 + i) for i in range(2)]
+    host = Context(0)
+    try:
+        ref, _ = host.detect_batch(imgs)
+    finally:
+        host.close()
+    want = b"".join(k.tobytes() for k in ref)
+    n = sum(len(k) for k in ref)
+    assert len(ref[0]) > 2 * 8192  # more than the fresh export buffers hold
+    ctx = Context(0)
+    try:
+        for job in range(3):  # bulk (fresh buffers), then exported, then async
+            t = ctx.submit(imgs, INPUT_F64_HOST, 1600, 1200, 1)
+            out = torch.full((n + 5, 168), 0xAB, dtype=torch.uint8, device=dev)
+            if job < 2:
+                counts = ctx.fetch_device(t, out.data_ptr(), n + 5)
+            else:
+                chk = torch.zeros(1, dtype=torch.int64, device=dev)
+                counts = ctx.fetch_device_async(t, out.data_ptr(), n + 5,
+                                                torch.cuda.current_stream().cuda_stream,
+                                                chk.data_ptr())
+            torch.cuda.synchronize()
+            assert counts == [len(k) for k in ref]
+            assert out[:n].cpu().numpy().tobytes() == want, job
+            assert bool((out[n:] == 0xAB).all())  # nothing written past the records
+            if job == 2:
+                assert int(chk.item()) == int(out[:n].view(-1).view(torch.int64).sum().item())
+    finally:
+        ctx.close()

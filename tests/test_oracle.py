@@ -87,3 +87,21 @@ def test_parameter_cases_are_pinned_to_the_reference():
         m = g.meta
         assert (m["w"], m["h"], m["c"], m["seed"]) == (w, h, c, zlib.crc32(name.encode()) & 0xFFFF)
         assert g.params() == p, name
+
+
+@pytest.mark.parametrize("g", all_goldens(kinds=("big",)), ids=lambda g: g.name)
+def test_big_goldens_full_arrays_consistent(g):
+    """Configs 3 and 5 keep every keypoint's u8 descriptor and pori (the
+    GPU test compares all of them); they must agree with the 64 full records
+    and the descriptor-float samples the same reference run wrote."""
+    desc, pori = g.full_desc_u8(), g.full_pori()
+    n = g.meta["final"]
+    assert desc.shape == (n, 128) and pori.shape == (n,)
+    assert np.array_equal(desc[g.sample_idx], g.final["desc"])
+    assert np.array_equal(pori[g.sample_idx].view(np.uint64), g.final["pori"].view(np.uint64))
+    sidx, sdf = g.strat_sample()
+    assert len(sidx) == min(4096, n) and np.all(np.diff(sidx) > 0)
+    # quantisation of the floats the reference wrote (sift.cpp:600-601)
+    q = np.minimum(np.floor(512.0 * sdf.astype(np.float64)), 255)
+    assert np.mean(np.abs(q - desc[sidx]) <= 1) == 1.0
+    assert np.all((pori >= 0) & (pori < 2 * np.pi))

@@ -94,6 +94,23 @@ def test_compose_and_canvas_chain():
     assert np.allclose(T[:2, 2], [100.0, 0.0])
 
 
+def test_canvas_clips_around_the_centre_image():
+    # a 6000-px-wide centre image far from the origin keeps its whole extent
+    # when a neighbour flies off; the clip window is centred on it
+    ims = [np.zeros((100, 6000, 3), np.uint8), np.zeros((100, 100, 3), np.uint8)]
+    far = np.array([[1, 0, 1e6], [0, 1, 0], [0, 0, 1.0]])
+    Hs = {0: np.array([[1, 0, 20000.0], [0, 1, 0], [0, 0, 1]]), 1: far}
+    T, W, H = canvas_for(ims, Hs, max_side=8192)
+    assert W <= 8192 and H == 100
+    lo = -T[0, 2]
+    assert lo <= 20000 and lo + W - 1 >= 20000 + 5999   # centre image fully inside
+    # every image (the centre included) projected behind the camera: the
+    # centre image's own box, no exception
+    behind = np.array([[1, 0, 0], [0, 1, 0], [0, 0, -1.0]])
+    T, W, H = canvas_for(ims, {0: behind, 1: behind})
+    assert (W, H) == (6000, 100) and np.allclose(T[:2, 2], [0.0, 0.0])
+
+
 # ---- GPU (HIP through the C-ABI) --------------------------------------------
 @pytest.mark.gpu
 def test_gpu_ransac_scores_and_model_equal_oracle(gpu_ctx):

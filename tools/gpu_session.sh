@@ -1,10 +1,52 @@
 #!/bin/bash
-# GPU session script (run from the repo root on the GPU box)
+# GPU session (run on the GPU box from the repo root):
+#   tools/gpu_session.sh <name> [test|bench|prof]...
+# test   pytest -m gpu (one process, per-test timeout)
+# bench  the driver's exact bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5)
+# prof   rocprofv3 --kernel-trace --stats of that same command, plus a
+#        serialised (SIFT_SERIAL=1, kernel-alone) trace; summaries via prof_summary.py
+# Every GPU step has its own time limit and the steps stop at the first failure.
 set -o pipefail
 R=$(pwd)
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "not slow" 2>&1 | tee gpurun_out/pytest_gpu.log || exit 1
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 2>&1 | tee gpurun_out/bench.log || exit 1
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $R/gpurun_out/bench_prof.log 2>&1 || exit 1
-echo DONE
+N=${1:?name}
+shift
+O=gpurun_out/$N
+mkdir -p $O
+for step in "$@"; do
+  case $step in
+  test)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+    tail -2 $O/pytest_gpu.log ;;
+  bench)
+    timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err \
+        || { tail -20 $O/bench.err; exit 1; }
+    cat $O/bench.json ;;
+  prof)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $R/$O/prof -o run \
+        -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $R/$O/bench_prof.json 2> $R/$O/bench_prof.err \
+        || { tail -20 $R/$O/bench_prof.err; exit 1; }
+    SIFT_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $R/$O/ser -o run \
+        -- python3 $R/bench.py --sync --steps 200 --warmup 10 --no-cpu-baseline --no-extra --no-matcher \
+        --no-alone --no-desc-f64 > $R/$O/bench_ser.json 2> $R/$O/bench_ser.err \
+        || { tail -20 $R/$O/bench_ser.err; exit 1; }
+    cd $R
+    python tools/prof_summary.py $O/prof/run_kernel_trace.csv > $O/summary.txt
+    python tools/prof_summary.py $O/ser/run_kernel_trace.csv > $O/summary_serial.txt
+    cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv 2>/dev/null
+    cp $O/ser/run_kernel_stats.csv $O/kernel_stats_serial.csv 2>/dev/null
+    echo PROF_DONE ;;
+  ab|ab2|ab3)
+    # interleaved A/B; variants and options from $AB_ARGS (resp. $AB2_ARGS, $AB3_ARGS)
+    v=AB_ARGS; [ $step = ab2 ] && v=AB2_ARGS; [ $step = ab3 ] && v=AB3_ARGS
+    timeout -k 10 600 python -u tools/ab_interleaved.py ${!v} > $O/$step.txt 2>&1 \
+        || { tail -20 $O/$step.txt; exit 1; }
+    grep -v amdgpu.ids $O/$step.txt ;;
+  divcheck)
+    timeout -k 10 300 tools/divcheck > $O/divcheck.txt 2>&1 || { tail -5 $O/divcheck.txt; exit 1; }
+    tail -3 $O/divcheck.txt ;;
+  *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo SESSION_DONE
