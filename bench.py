@@ -358,6 +358,9 @@ def main() -> int:
     ap.add_argument("--exchange", action="store_true",
                     help="run the RCCL record exchange also at world size 1 (tests the N>1 "
                          "data path on one GPU)")
+    ap.add_argument("--exchange-steps", type=int, default=8,
+                    help="steps whose records share one all-gather (RCCL's per-call host "
+                         "cost amortised over a bucket of steps)")
     ap.add_argument("--sync", action="store_true",
                     help="one job at a time (no pipelining), for profiling / A-B")
     ap.add_argument("--no-desc-f64", action="store_true",
@@ -460,8 +463,9 @@ def main() -> int:
     kp_per_image = ctx.counts()["final_n"] // B
     if use_exchange:
         from sift_dist import RecordExchange, agree_capacity
-        exchange = RecordExchange(agree_capacity(max_rows, dev), dev, max_images=max(16, B),
-                                  verify_ctx=ctx)
+        exchange = RecordExchange(agree_capacity(max_rows * args.exchange_steps, dev), dev,
+                                  max_images=max(16, B), verify_ctx=ctx,
+                                  steps_per_exchange=args.exchange_steps)
         run(1)  # one untimed pipelined step
 
     if world > 1:
@@ -508,6 +512,7 @@ def main() -> int:
         exchange_check = {"records_match_peer_redetect": bool(chk[0]),
                           "min_images_received_per_rank": int(chk[1]),
                           "images_per_step": world * B,
+                          "steps_per_exchange": args.exchange_steps,
                           "slots_checksummed": int(chk[3]),
                           "slot_checksum_mismatches": int(chk[2]),
                           "note": "every step: each received slot's records summed on the device "
@@ -570,7 +575,8 @@ def main() -> int:
                 "keypoints_per_image": kp_per_image,
                 "parallelism": f"image-sharded x{world}" + (
                     ", RCCL all-gather of the descriptor records straight from HBM "
-                    "(sift_hip_fetch_device), pipelined one step behind" if world > 1 else ""),
+                    f"(sift_hip_fetch_device_async), one collective per {args.exchange_steps} "
+                    "steps, overlapping the next steps" if use_exchange else ""),
             },
             "roofline": roofline,
             "extrema_roofline": extrema_roofline,

@@ -187,14 +187,16 @@ int sift_hip_fetch_device_async(sift_ctx* ctx, int ticket, void* d_out, size_t c
 
 /* Exchange verification for the multi-GPU driver: n_slots slots of
  * slot_bytes each at d_slots (device memory); slot r holds at 8-byte word
- * count_word its record count n and at word sum_word the sender's checksum
- * (sift_hip_fetch_device_async), with the n 168-byte records after hdr_rows
- * header rows of 168 bytes. Every slot whose records do not sum to its
- * checksum (or whose n exceeds cap_rows) adds 1 to *d_bad (device memory).
- * Enqueued on `stream` (default: the context's), no host wait. */
+ * count_word its record count n, at words [sum_word, sum_word + n_sum_words)
+ * the sender's checksums of consecutive pieces of its records (one
+ * sift_hip_fetch_device_async each), and the n 168-byte records after
+ * hdr_rows header rows of 168 bytes. Every slot whose records' wrapping word
+ * sum differs from the sum of its checksums (or whose n exceeds cap_rows)
+ * adds 1 to *d_bad (device memory). Enqueued on `stream` (default: the
+ * context's), no host wait. */
 int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_t slot_bytes,
-                          int hdr_rows, int count_word, int sum_word, size_t cap_rows,
-                          uint64_t* d_bad, void* stream);
+                          int hdr_rows, int count_word, int sum_word, int n_sum_words,
+                          size_t cap_rows, uint64_t* d_bad, void* stream);
 
 /* submit + wait + fetch into library-allocated storage (sift_hip_free):
  * *out_kps image-major, counts[b] per image. */

@@ -1267,17 +1267,19 @@ int sift_hip_fetch_device_async(sift_ctx* ctx, int ticket, void* d_out, size_t c
 }
 
 int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_t slot_bytes,
-                          int hdr_rows, int count_word, int sum_word, size_t cap_rows,
-                          uint64_t* d_bad, void* stream) {
+                          int hdr_rows, int count_word, int sum_word, int n_sum_words,
+                          size_t cap_rows, uint64_t* d_bad, void* stream) {
     if (!ctx || !d_bad || (n_slots > 0 && !d_slots) || n_slots < 0 || hdr_rows < 0 ||
-        count_word < 0 || sum_word < 0 || slot_bytes % 8 ||
-        (size_t)(count_word + 1) * 8 > slot_bytes || (size_t)(sum_word + 1) * 8 > slot_bytes ||
+        count_word < 0 || sum_word < 0 || n_sum_words < 1 || slot_bytes % 8 ||
+        (size_t)(count_word + 1) * 8 > slot_bytes ||
+        (size_t)(sum_word + n_sum_words) * 8 > slot_bytes ||
         ((size_t)hdr_rows + cap_rows) * sizeof(sift_kp) > slot_bytes)
         return SIFT_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     SIFT_HIP_TRY(launch_verify_slots(d_slots, n_slots, slot_bytes, hdr_rows, count_word, sum_word,
-                                     cap_rows, reinterpret_cast<unsigned long long*>(d_bad), st));
+                                     n_sum_words, cap_rows,
+                                     reinterpret_cast<unsigned long long*>(d_bad), st));
     return SIFT_OK;
 }
 

@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "sift_pow2.h"
 #include "sift_kernels.h"
 
 // compile-time A/B knobs (alternative builds, SIFT_HIP_LIB)
@@ -1068,8 +1069,8 @@ __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict_
 // ---------------------------------------------------------------------------
 // refine_one: compute_keypoints (sift.cpp:330-436) for one candidate, with
 // get_pixel_cube, compute_gradient, compute_hessian, fit_quadratic
-// (sift.cpp:32-106); bit-exact (no libm except the size's pow(2, t), which
-// the host recomputes with glibc for the final records).
+// (sift.cpp:32-106); bit-exact (no libm: the size's pow(2, t) is glibc's
+// algorithm, sift_pow2.h).
 // ---------------------------------------------------------------------------
 __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, int ex, int ey,
                            int ez, int o, int im, RawKp* out) {
@@ -1136,7 +1137,9 @@ __device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, 
     const double scale = pow2i(o);
     out->x = scale * (x + off1);
     out->y = scale * (y + off2);
-    out->size = P.init_sigma * scale * pow(2.0, ((double)layer + off0) / P.intervals);
+    // glibc's pow(2, t), bit for bit (sift_pow2.h): the size sets the
+    // orientation and descriptor windows, so it must be the reference's
+    out->size = P.init_sigma * scale * pow2_glibc(((double)layer + off0) / P.intervals);
     out->off0 = off0;
     out->octave = o;
     out->layer = layer;
@@ -2036,12 +2039,14 @@ hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, u
 }
 
 // Exchange verification (sift_hip_verify_slots): slot r of `slots` holds,
-// from word `count_word`, the number of 168-B records after `hdr_rows`
-// header rows, and at word `sum_word` the sender's checksum of them
-// (k_gather_records). One workgroup per slot; a mismatch increments *bad.
+// at word `count_word`, the number of 168-B records after `hdr_rows` header
+// rows, and at words [sum_word, sum_word + n_sums) the sender's checksums of
+// consecutive pieces of them (k_gather_records, one per step); the records'
+// wrapping word sum must equal the checksums' sum. One workgroup per slot; a
+// mismatch increments *bad.
 __global__ __launch_bounds__(256) void k_verify_slots(const unsigned long long* __restrict__ slots,
                                                       size_t slot_words, int hdr_rows,
-                                                      int count_word, int sum_word,
+                                                      int count_word, int sum_word, int n_sums,
                                                       size_t cap_rows,
                                                       unsigned long long* __restrict__ bad) {
     __shared__ unsigned long long part[4];
@@ -2054,18 +2059,20 @@ __global__ __launch_bounds__(256) void k_verify_slots(const unsigned long long* 
     v = wave_sum_u64(v);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0 &&
-        (n > cap_rows || part[0] + part[1] + part[2] + part[3] != sl[sum_word]))
-        atomicAdd(bad, 1ull);
+    if (threadIdx.x == 0) {
+        unsigned long long want = 0;
+        for (int k = 0; k < n_sums; ++k) want += sl[sum_word + k];
+        if (n > cap_rows || part[0] + part[1] + part[2] + part[3] != want) atomicAdd(bad, 1ull);
+    }
 }
 
 hipError_t launch_verify_slots(const void* slots, int n_slots, size_t slot_bytes, int hdr_rows,
-                               int count_word, int sum_word, size_t cap_rows,
+                               int count_word, int sum_word, int n_sums, size_t cap_rows,
                                unsigned long long* bad, hipStream_t s) {
     if (n_slots <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_verify_slots, dim3(n_slots), dim3(256), 0, s,
                        static_cast<const unsigned long long*>(slots), slot_bytes / 8, hdr_rows,
-                       count_word, sum_word, cap_rows, bad);
+                       count_word, sum_word, n_sums, cap_rows, bad);
     return hipGetLastError();
 }
 

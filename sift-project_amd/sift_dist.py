@@ -83,41 +83,48 @@ class RecordExchange:
     """Pipelined all-gather of per-step record buffers for a steady stream of
     batches (the multi-GPU bench path).
 
-    One collective per step, no count exchange and no host synchronisation:
-    every rank sends a fixed-capacity slot (`cap_rows` records of 168 B after
-    header rows holding the image count, the record count and per-image
-    (image id, record count) pairs for up to `max_images` images), with
-    ``all_gather_into_tensor`` issued asynchronously on a side stream, so
-    step i's exchange overlaps step i+1's detection. Slots are
-    double-buffered; a slot is refilled only after the collective that last
-    read it has completed. `cap_rows` must be the same on every rank (see
-    ``agree_capacity``). Every rank always takes part in the same collective
-    (no per-rank fallback that could diverge): a slot that overflows is sent
-    truncated with its true count, and ``result`` raises for it;
-    ``allgather_records`` is the exact two-phase exchange for callers that
-    cannot bound the counts.
+    No count exchange and no host synchronisation on the data path: every
+    rank sends a fixed-capacity slot (`cap_rows` records of 168 B after
+    header rows) with ``all_gather_into_tensor`` issued asynchronously on a
+    side stream, so the exchange overlaps the following steps' detection.
+    A slot collects the records of `steps_per_exchange` consecutive steps
+    (one collective per bucket of steps: RCCL's per-call host cost is
+    amortised; xGMI moves larger messages at the same per-link rate), and
+    slots are double-buffered: a slot is refilled only after the collective
+    that last read it has completed. `cap_rows` (per slot, i.e. per bucket of
+    steps) must be the same on every rank (see ``agree_capacity``). Every
+    rank always takes part in the same collectives (no per-rank fallback that
+    could diverge): a slot that overflows is sent truncated with its true
+    count, and ``result`` raises for it; ``allgather_records`` is the exact
+    two-phase exchange for callers that cannot bound the counts.
+
+    Header words: entry count, record count, (image id, record count) per
+    entry (up to max_images per step), then one checksum per step: the
+    wrapping 64-bit sum of that step's record words, written by the sender
+    (on the device by the library under RCCL, on the host under gloo). Every
+    received slot is checked against its checksums once its collective has
+    completed (on the device with `verify_ctx`, a sift_hip.Context;
+    ``mismatches`` reads the count).
 
     ``push`` takes host buffers (staged through pinned memory); ``push_device``
     takes a submitted detect job and has the library write its final records
-    straight into the device slot (sift_hip_fetch_device: gathered on the GPU
-    from the records in HBM), so the payload never crosses PCIe.
+    straight into the device slot (sift_hip_fetch_device_async: gathered on
+    the GPU from the records in HBM, ordered before the collective by an
+    event), so the payload never crosses PCIe.
     """
 
     def __init__(self, cap_rows: int, device: torch.device, group=None, max_images: int = 16,
-                 verify_ctx=None):
+                 verify_ctx=None, steps_per_exchange: int = 1):
         self.group = group
         self.world = dist.get_world_size(group)
         self.cap = int(cap_rows)
         self.device = device
         self.cuda = device.type == "cuda"
         self.max_images = int(max_images)
-        # header words: image count, record count, (image id, count) per
-        # image, then the sender's checksum of its records (the wrapping
-        # 64-bit sum of their 8-byte words): every received slot of every
-        # step is checked against it (on the device with `verify_ctx`, a
-        # sift_hip.Context, under RCCL; on the host under gloo)
-        self.sum_word = 2 + 2 * self.max_images
-        self.hdr_words = self.sum_word + 1
+        self.bucket = max(1, int(steps_per_exchange))
+        self.max_entries = self.max_images * self.bucket
+        self.sum_word = 2 + 2 * self.max_entries
+        self.hdr_words = self.sum_word + self.bucket
         self.hdr_rows = math.ceil(self.hdr_words * 8 / RECORD_BYTES)
         self.verify_ctx = verify_ctx
         self.bad = torch.zeros(1, dtype=torch.int64, device=device)
@@ -133,7 +140,15 @@ class RecordExchange:
         self.stream = torch.cuda.Stream(device) if self.cuda else None
         self.done = [None, None]  # per slot: event (cuda) / work handle (cpu)
         self.work = [None, None]
-        self.step = 0
+        self.step = 0        # collectives started
+        self.cur = None      # slot being filled
+        self._reset_fill()
+
+    def _reset_fill(self):
+        self.fill = 0        # records in the current slot (truncated at cap)
+        self.total = 0       # records pushed into it (true count)
+        self.entries = []    # (image id, count)
+        self.n_steps = 0     # steps in the current slot
 
     def _wait_slot(self, s: int) -> None:
         if self.done[s] is not None:
@@ -152,35 +167,60 @@ class RecordExchange:
             w = g[r].view("<u8")
             n = int(w[1])
             recs = w[self.hdr_rows * RECORD_BYTES // 8:][: min(n, self.cap) * RECORD_BYTES // 8]
-            if n > self.cap or int(recs.sum(dtype="<u8")) != int(w[self.sum_word]):
+            want = w[self.sum_word:self.sum_word + self.bucket].sum(dtype="<u8")
+            if n > self.cap or int(recs.sum(dtype="<u8")) != int(want):
                 self.bad += 1
         self.checked += self.world
 
-    def _next_slot(self) -> int:
-        s = self.step & 1
-        self.step += 1
-        self._wait_slot(s)
-        return s
+    def _open_slot(self) -> int:
+        """The slot the next step writes into (claimed at a bucket's first
+        step, once the collective that last read it has completed)."""
+        if self.cur is None:
+            s = self.step & 1
+            self._wait_slot(s)
+            self.cur = s
+            self._reset_fill()
+            if not self.cuda:  # unused checksum words of a short bucket read as 0
+                self.host[s].view(-1)[self.sum_word * 8:self.hdr_words * 8] = 0
+        return self.cur
 
-    def _header(self, counts: Sequence[int], image_ids: Sequence[int]) -> torch.Tensor:
-        """The header words before the checksum (host-built)."""
-        if len(counts) > self.max_images:
-            raise ValueError(f"{len(counts)} images per step > max_images={self.max_images}")
+    def _header(self) -> torch.Tensor:
+        """The host-built header words (before the per-step checksums)."""
         hdr = torch.zeros(self.sum_word, dtype=torch.int64)
-        hdr[0] = len(counts)
-        hdr[1] = sum(int(c) for c in counts)
-        for j, (c, i) in enumerate(zip(counts, image_ids)):
+        hdr[0] = len(self.entries)
+        hdr[1] = self.total
+        for j, (i, c) in enumerate(self.entries):
             hdr[2 + 2 * j] = int(i)
             hdr[3 + 2 * j] = int(c)
         return hdr.view(torch.uint8)
 
-    def _launch(self, s: int, n_host_bytes: int) -> None:
-        """Copy the slot's first n_host_bytes from its pinned staging and
-        start the all-gather (async on the side stream for cuda)."""
+    def _add_entries(self, counts: Sequence[int], image_ids: Sequence[int]) -> None:
+        if len(counts) > self.max_images:
+            raise ValueError(f"{len(counts)} images per step > max_images={self.max_images}")
+        self.entries += [(int(i), int(c)) for c, i in zip(counts, image_ids)]
+        self.total += sum(int(c) for c in counts)
+        self.n_steps += 1
+
+    def _finish_step(self) -> int:
+        """Close the step; start the collective when the bucket is full.
+        Returns the slot index (its result is valid once flushed)."""
+        s = self.cur
+        if self.n_steps == self.bucket:
+            self._launch()
+        return s
+
+    def _launch(self) -> None:
+        """Copy the slot's host-written bytes from pinned staging and start
+        the all-gather (async on the side stream for cuda)."""
+        s = self.cur
+        hdr = self._header()
+        h = self.host[s]
+        h.view(-1)[: hdr.numel()] = hdr
+        n_host_bytes = hdr.numel() if self.cuda else (self.hdr_rows + self.fill) * RECORD_BYTES
         if self.cuda:
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.stream):
-                self.dev[s].view(-1)[:n_host_bytes].copy_(self.host[s].view(-1)[:n_host_bytes],
+                self.dev[s].view(-1)[:n_host_bytes].copy_(h.view(-1)[:n_host_bytes],
                                                           non_blocking=True)
                 self.work[s] = dist.all_gather_into_tensor(self.gathered[s], self.dev[s],
                                                            group=self.group, async_op=True)
@@ -189,74 +229,86 @@ class RecordExchange:
                     rows = self.cap + self.hdr_rows
                     self.verify_ctx.verify_slots(
                         self.gathered[s].data_ptr(), self.world, rows * RECORD_BYTES,
-                        self.hdr_rows, 1, self.sum_word, self.cap, self.bad.data_ptr(),
-                        self.stream.cuda_stream)
+                        self.hdr_rows, 1, self.sum_word, self.bucket, self.cap,
+                        self.bad.data_ptr(), self.stream.cuda_stream)
                     self.checked += self.world
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
                 self.done[s] = ev
         else:
-            self.dev[s].view(-1)[:n_host_bytes] = self.host[s].view(-1)[:n_host_bytes]
+            self.dev[s].view(-1)[:n_host_bytes] = h.view(-1)[:n_host_bytes]
             self.work[s] = dist.all_gather_into_tensor(self.gathered[s], self.dev[s],
                                                        group=self.group, async_op=True)
             self.done[s] = self.work[s]
+        self.step += 1
+        self.cur = None
 
     def push(self, local: Sequence[torch.Tensor], image_ids: Sequence[int]) -> int:
-        """Start the exchange of this step's buffers (uint8 [n_i, 168], host);
+        """Add this step's buffers (uint8 [n_i, 168], host) to the exchange;
         returns the slot index whose `gathered` buffer will hold the result."""
-        s = self._next_slot()
+        s = self._open_slot()
         h = self.host[s]
-        hdr = self._header([int(t.shape[0]) for t in local], image_ids)
-        h.view(-1)[: hdr.numel()] = hdr
-        off = self.hdr_rows
+        k = self.n_steps
+        self._add_entries([int(t.shape[0]) for t in local], image_ids)
+        off0 = self.hdr_rows + self.fill
+        off = off0
         for t in local:  # a slot that overflows is truncated and flagged
             n = min(int(t.shape[0]), self.cap + self.hdr_rows - off)
             h[off: off + n] = t[:n]
             off += n
-        words = h[self.hdr_rows: off].numpy().view("<u8")
-        h.view(-1)[self.sum_word * 8:(self.sum_word + 1) * 8] = torch.from_numpy(
+        self.fill = off - self.hdr_rows
+        words = h[off0: off].numpy().view("<u8")
+        h.view(-1)[(self.sum_word + k) * 8:(self.sum_word + k + 1) * 8] = torch.from_numpy(
             np.array([words.sum(dtype="<u8")], dtype="<u8").view(np.uint8))
-        self._launch(s, off * RECORD_BYTES)
-        return s
+        return self._finish_step()
 
     def push_device(self, sift_ctx, ticket: int, image_ids: Sequence[int]) -> int:
-        """Start the exchange of a submitted detect job's records: the
-        library writes them into the device slot (no host copy of the
-        payload; only the header goes through pinned staging)."""
+        """Add a submitted detect job's records to the exchange: the library
+        writes them into the device slot (no host copy of the payload; only
+        the header goes through pinned staging) and their checksum into the
+        step's header word."""
         counts = sift_ctx.wait(ticket)
         n_rows = sum(counts)
-        s = self._next_slot()
-        base = self.dev[s][self.hdr_rows:]
-        chk = self.dev[s].view(-1)[self.sum_word * 8:(self.sum_word + 1) * 8]
-        if n_rows <= self.cap:
+        s = self._open_slot()
+        k = self.n_steps
+        base = self.dev[s][self.hdr_rows + self.fill:]
+        room = self.cap - self.fill
+        chk = self.dev[s].view(-1)[(self.sum_word + k) * 8:(self.sum_word + k + 1) * 8]
+        if n_rows <= room:
             # gathered on the library's stream; the side stream waits on it
-            # with an event (no host synchronisation), and the library adds
-            # the records' word sum into the slot's checksum word
-            sift_ctx.fetch_device_async(ticket, base.data_ptr(), self.cap,
-                                        self.stream.cuda_stream, chk.data_ptr())
+            # with an event (no host synchronisation)
+            sift_ctx.fetch_device_async(ticket, base.data_ptr(), room, self.stream.cuda_stream,
+                                        chk.data_ptr())
+            self.fill += n_rows
         else:  # overflow: truncated and flagged, as push does
             cur = torch.cuda.current_stream(self.device)
             tmp = torch.empty((n_rows, RECORD_BYTES), dtype=torch.uint8, device=self.device)
             sift_ctx.fetch_device_async(ticket, tmp.data_ptr(), n_rows, cur.cuda_stream)
-            base.copy_(tmp[: self.cap])
-            w = base.view(-1).view(torch.int64)  # torch sums int64 with wrap-around
+            base[:room].copy_(tmp[:room])
+            w = base[:room].reshape(-1).view(torch.int64)  # torch sums int64 with wrap-around
             chk.view(torch.int64).copy_(w.sum().view(1))
-        hdr = self._header(counts, image_ids)
-        self.host[s].view(-1)[: hdr.numel()] = hdr
-        self._launch(s, hdr.numel())
-        return s
+            self.fill = self.cap
+        self._add_entries(counts, image_ids)
+        return self._finish_step()
+
+    def flush(self) -> None:
+        """Start the collective of a partly filled bucket, then wait for
+        every exchange in flight."""
+        if self.cur is not None and self.n_steps > 0:
+            if self.cuda:  # checksum words of the bucket's missing steps
+                self.dev[self.cur].view(-1)[(self.sum_word + self.n_steps) * 8:
+                                            self.hdr_words * 8].zero_()
+            self._launch()
+        for s in (0, 1):
+            self._wait_slot(s)
 
     def mismatches(self) -> int:
-        """Slots (one per rank per completed step) whose records did not sum
-        to their sender's checksum; call flush first."""
+        """Received slots whose records did not sum to their senders'
+        checksums (one check per rank per completed collective); call flush
+        first."""
         if self.cuda:
             torch.cuda.synchronize(self.device)
         return int(self.bad.item())
-
-    def flush(self) -> None:
-        """Wait for every exchange in flight."""
-        for s in (0, 1):
-            self._wait_slot(s)
 
     def result(self, s: int) -> Dict[int, torch.Tensor]:
         """{image_id: uint8 [n, 168]} of a completed slot (call flush first)."""

@@ -190,8 +190,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sift_hip_wait.argtypes = [vp, i, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     lib.sift_hip_fetch.argtypes = [vp, i, vp, vp]
     lib.sift_hip_fetch_device.argtypes = [vp, i, vp, sz]
-    lib.sift_hip_fetch_device_async.argtypes = [vp, i, vp, sz, vp, vp]
-    lib.sift_hip_verify_slots.argtypes = [vp, vp, i, sz, i, i, i, sz, vp, vp]
+    if hasattr(lib, "sift_hip_fetch_device_async"):  # (absent from older A/B builds)
+        lib.sift_hip_fetch_device_async.argtypes = [vp, i, vp, sz, vp, vp]
+        lib.sift_hip_verify_slots.argtypes = [vp, vp, i, sz, i, i, i, i, sz, vp, vp]
     lib.sift_hip_detect_batch.argtypes = [vp, ctypes.POINTER(vp), i, i, i, i, i,
                                           ctypes.POINTER(CParams), ctypes.POINTER(vp),
                                           ctypes.POINTER(sz), ctypes.POINTER(vp)]

@@ -164,3 +164,50 @@ def test_record_exchange_many_images_gloo():
     want = {i: _records(7, i, 3 + i % 5).tobytes() for i in range(12 * world)}
     for r in range(world):
         assert res[r] == want
+
+
+def _bucket_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids = shard(2 * world, rank, world)
+        ex = RecordExchange(3 * 64, torch.device("cpu"), steps_per_exchange=3)
+        slots = []
+        for step in range(4):  # one full bucket of 3 steps, then one flushed alone
+            bufs = [torch.from_numpy(_records(step, i, 5 + step + rank)) for i in ids]
+            slots.append(ex.push(bufs, ids))
+        ex.flush()
+        # the first bucket's slot was overwritten by no later collective
+        got = {k: v.numpy().tobytes() for k, v in ex.result(slots[0]).items()}
+        last = {k: v.numpy().tobytes() for k, v in ex.result(slots[3]).items()}
+        out_q.put((rank, got, last, ex.step, ex.checked, ex.mismatches()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_record_exchange_bucketed_gloo():
+    """steps_per_exchange = 3: three steps' records share one collective (the
+    last bucket's image ids win in result()); a partial bucket is sent by
+    flush; every received slot passes its per-step checksums."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got, last, n_coll, checked, bad = q.get(timeout=120)
+        res[r] = (got, last)
+        assert (n_coll, checked, bad) == (2, 2 * world, 0)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        got, last = res[r]
+        for rr in range(world):
+            for i in shard(2 * world, rr, world):
+                assert got[i] == _records(2, i, 5 + 2 + rr).tobytes()
+                assert last[i] == _records(3, i, 5 + 3 + rr).tobytes()

@@ -225,6 +225,17 @@ def test_gpu_batch_record_exchange_world1(gpu_ctx):
                 assert res[i].cpu().numpy().tobytes() == kps[i].tobytes(), (step, i)
         # every received slot of every step matched its sender's checksum
         assert ex.checked == 4 and ex.mismatches() == 0
+        # two steps per collective: both steps' records in one slot
+        exb = RecordExchange(8192, dev, verify_ctx=gpu_ctx, steps_per_exchange=2)
+        for step in range(3):  # one full bucket, then a partial one sent by flush
+            t = gpu_ctx.submit(imgs, INPUT_F64_HOST, 480, 360, 1)
+            s = exb.push_device(gpu_ctx, t, [10 * step + i for i in ids])
+        exb.flush()
+        first, last = exb.result(0), exb.result(s)
+        for step, res in ((0, first), (1, first), (2, last)):
+            for i in ids:
+                assert res[10 * step + i].cpu().numpy().tobytes() == kps[i].tobytes(), (step, i)
+        assert exb.step == 2 and exb.checked == 2 and exb.mismatches() == 0
         # too small a destination keeps the job; then it can still be fetched
         t = gpu_ctx.submit(imgs[:1], INPUT_F64_HOST, 480, 360, 1)
         small = torch.empty((1, RECORD_BYTES), dtype=torch.uint8, device=dev)

@@ -71,6 +71,26 @@ def check_big_golden(ctx, g):
     r = compare_final(kps, None, ref, None)
     r["desc_f32_max"] = float(np.max(np.abs(df[sidx].astype(np.float64) - sdf)))
     assert final_ok(r), r
+    # the size the DEVICE computed (it sets the orientation and descriptor
+    # windows) equals the reference's glibc size for every keypoint: the
+    # kernels' own records, before the host's finalisation, matched to the
+    # final ones by (x, y, octave, layer, pori)
+    import torch
+
+    n = ctx.n_records()
+    buf = torch.empty((n, 168), dtype=torch.uint8, device="cuda:0")
+    assert ctx.copy_records_device(buf.data_ptr(), n) == n
+    dev = np.frombuffer(buf.cpu().numpy().tobytes(), dtype=kps.dtype)
+    key = lambda a: np.stack([a["x"].view(np.uint64), a["y"].view(np.uint64),  # noqa: E731
+                              a["octave"].astype(np.uint64), a["layer"].astype(np.uint64),
+                              a["pori"].view(np.uint64)], axis=1)
+    kd, kf = key(dev), key(kps)
+    order = np.lexsort(kd.T[::-1])
+    pos = np.searchsorted(np.ascontiguousarray(kd[order]).view([("", np.uint64)] * 5).ravel(),
+                          np.ascontiguousarray(kf).view([("", np.uint64)] * 5).ravel())
+    match = order[np.minimum(pos, n - 1)]
+    assert np.array_equal(kd[match], kf)
+    assert np.array_equal(dev["size"][match].view(np.uint64), kps["size"].view(np.uint64))
     return r
 
 
