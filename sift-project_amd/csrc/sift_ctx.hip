@@ -646,6 +646,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         const int gb = n_batches++;
         const int L = gb % lanes;
         for (hipStream_t sp : sps) {
+            if (sp == lane_stream[L]) continue;  // same stream: already ordered
             hipEvent_t pyr_done = sync_event(s);
             if (!pyr_done) return SIFT_ERR_HIP;
             SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
@@ -659,7 +660,10 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // octave o (the small octaves are latency-bound: two in flight at once).
     hipStream_t pyr[2] = {sA, sB};
     hipEvent_t base_ready = nullptr;  // next octave's base written (decimation)
-    if (o_small > 0 || o_small < g.octaves) {
+    // cross-stream events only where the two pyramid streams differ (a job
+    // on one stream is ordered by the stream itself: fewer API calls)
+    const bool two_pyr = sA != sB;
+    if (two_pyr && (o_small > 0 || o_small < g.octaves)) {
         // stream B's first octave must also see the input staging on A
         base_ready = sync_event(s);
         if (!base_ready) return SIFT_ERR_HIP;
@@ -667,12 +671,12 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     }
     for (int o = 0; o < o_small; ++o) {
         hipStream_t so = pyr[o & 1];
-        if (o > 0) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
+        if (o > 0 && two_pyr) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
         for (int l = 1; l < g.n_gauss; ++l) {
             const bool dec = (l == dec_level) && (o + 1 < g.octaves);
             if ((st = blur(so, o, l, s.h_pt.lvl[o][l - 1], stride, s.taps[l], dec)) != SIFT_OK)
                 return st;
-            if (dec) {
+            if (dec && two_pyr) {
                 base_ready = sync_event(s);
                 if (!base_ready) return SIFT_ERR_HIP;
                 SIFT_HIP_TRY(hipEventRecord(base_ready, so));
@@ -682,7 +686,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     }
     if (o_small < g.octaves) {
         hipStream_t so = pyr[o_small & 1];
-        SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
+        if (two_pyr) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
         double bytes = 0.0;
         for (int o = o_small; o < g.octaves; ++o) {
             bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[o] * (double)g.H[o];
@@ -697,7 +701,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
     // lane D joins C, then the live counters come back on C: the job's last
     // device work (the final batch waited on both pyramid streams)
-    {
+    if (sD != sC) {
         hipEvent_t jd = sync_event(s);
         if (!jd) return SIFT_ERR_HIP;
         SIFT_HIP_TRY(hipEventRecord(jd, sD));

@@ -1072,29 +1072,44 @@ __global__ __launch_bounds__(256) void k_extrema_any(const PyrTable* __restrict_
 // (sift.cpp:32-106); bit-exact (no libm: the size's pow(2, t) is glibc's
 // algorithm, sift_pow2.h).
 // ---------------------------------------------------------------------------
-__device__ bool refine_one(const PyrTable* __restrict__ pt, const DevParams& P, int ex, int ey,
-                           int ez, int o, int im, RawKp* out) {
+// The pyramid table in LDS: the plane bases every refine step looks up per
+// lane (a candidate's octave and layer vary across the wave), so a step
+// costs one round trip to memory (its 36 pixels), not two.
+struct RefineLds {
+    const double* lvl[kMaxOctaves][kMaxLevels];
+    int w[kMaxOctaves], h[kMaxOctaves];
+};
+
+__device__ bool refine_one(const RefineLds& T, size_t img_stride, const DevParams& P, int ex,
+                           int ey, int ez, int o, int im, RawKp* out) {
     const int b = P.window_size / 2;
-    const int W = pt->w[o], H = pt->h[o], depth = P.n_dog;
+    const int W = T.w[o], H = T.h[o], depth = P.n_dog;
     double x = ex, y = ey;
     int layer = ez;
     double off0 = 0, off1 = 0, off2 = 0;
     int step;
     for (step = 0; step < kMaxSteps; ++step) {
-        double c[3][3][3];
+        // the 3x3x3 DoG cube from the four Gaussian planes layer-1..layer+2:
+        // all 36 loads in flight together
         const int xi = (int)x, yi = (int)y;
+        double g[4][3][3];  // [plane][dy][dx]
 #pragma unroll
-        for (int dz = -1; dz <= 1; ++dz) {
-            gdouble* ga = gbl(plane(pt, im, o, layer + dz + 1));
-            gdouble* gb = gbl(plane(pt, im, o, layer + dz));
+        for (int pl = 0; pl < 4; ++pl) {
+            gdouble* gp = gbl(T.lvl[o][layer - 1 + pl] + (size_t)im * img_stride);
 #pragma unroll
-            for (int dx = -1; dx <= 1; ++dx)
+            for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-                for (int dy = -1; dy <= 1; ++dy) {
-                    const size_t q = (size_t)(yi + dy) * W + (xi + dx);
-                    c[dz + 1][dx + 1][dy + 1] = (ga[q] - gb[q]) / 255.0;
-                }
+                for (int dx = -1; dx <= 1; ++dx)
+                    g[pl][dy + 1][dx + 1] = gp[(size_t)(yi + dy) * W + (xi + dx)];
         }
+        double c[3][3][3];  // get_pixel_cube (sift.cpp:32-44): [layer][x][y], /255
+#pragma unroll
+        for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+                    c[dz][dx][dy] = (g[dz + 1][dy][dx] - g[dz][dy][dx]) / 255.0;
         const double g0 = 0.5 * (c[2][1][1] - c[0][1][1]);
         const double g1 = 0.5 * (c[1][2][1] - c[1][0][1]);
         const double g2 = 0.5 * (c[1][1][2] - c[1][1][0]);
@@ -1157,12 +1172,22 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
                                                 unsigned cap_cand, RawKp* __restrict__ out,
                                                 unsigned* __restrict__ n_out,
                                                 unsigned cap_out) {
+    __shared__ RefineLds T;
     const unsigned n = min(*n_cand, cap_cand);
     const unsigned i0 = min(*cand_begin, n);
+    const unsigned stride = gridDim.x * blockDim.x;
+    if (i0 + blockIdx.x * blockDim.x >= n) return;  // no candidate for this workgroup
     // grid-stride over whole waves (wave-uniform trip count), so the kept
     // keypoints of a wave take one counter atomic (ballot + prefix)
     const int lane = threadIdx.x & 63;
-    const unsigned stride = gridDim.x * blockDim.x;
+    for (int k = threadIdx.x; k < kMaxOctaves * kMaxLevels; k += 256)
+        T.lvl[k / kMaxLevels][k % kMaxLevels] = pt->lvl[k / kMaxLevels][k % kMaxLevels];
+    if (threadIdx.x < kMaxOctaves) {
+        T.w[threadIdx.x] = pt->w[threadIdx.x];
+        T.h[threadIdx.x] = pt->h[threadIdx.x];
+    }
+    const size_t img_stride = pt->img_stride;
+    __syncthreads();
     for (unsigned i0w = i0 + blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0w < n;
          i0w += stride) {
         const unsigned i = i0w + lane;
@@ -1171,7 +1196,7 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
         if (i < n) {
             const sift_extremum e = cand[i];
             const int o = e.octave & ((1 << kOctBits) - 1), im = e.octave >> kOctBits;
-            keep = refine_one(pt, P, e.x, e.y, e.z, o, im, &r);
+            keep = refine_one(T, img_stride, P, e.x, e.y, e.z, o, im, &r);
         }
         const unsigned long long m = __ballot(keep);
         if (m) {
@@ -1233,6 +1258,32 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
 //    reductions (the bins themselves are already summed out of the
 //    reference's order, so a sequential sum would buy no exactness).
 // ---------------------------------------------------------------------------
+// atan2 in f32 for the descriptor's sample math: octant reduction to
+// a = min(|x|, |y|) / max(|x|, |y|) (v_rcp_f32, 1 ulp), atan(a) as
+// a + a^3 p(a^2) with a degree-7 p fitted for minimum max error on [0, 1]
+// (8.5e-8 rad in f32 arithmetic over 2e6 points), then the quadrant fix-up.
+// About 20 VALU instructions against ~35 for atan2f; total error below
+// 2e-7 rad, i.e. < 3e-7 of a descriptor orientation bin (contract: 1e-4 on
+// the normalised floats). atan2(0, 0) = 0; signs of zeros as atan2f.
+__device__ __forceinline__ float atan2_f32(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float t = a * a;
+    float p = 0.0026222362648695707f;
+    p = fmaf(p, t, -0.015132501721382141f);
+    p = fmaf(p, t, 0.04112179949879646f);
+    p = fmaf(p, t, -0.0736670047044754f);
+    p = fmaf(p, t, 0.1057392954826355f);
+    p = fmaf(p, t, -0.1418597400188446f);
+    p = fmaf(p, t, 0.1999039649963379f);
+    p = fmaf(p, t, -0.33332985639572144f);
+    float th = fmaf(a * t, p, a);
+    if (ay > ax) th = 1.57079637f - th;
+    if (x < 0.0f) th = 3.14159274f - th;
+    return copysignf(th, y);
+}
+
 constexpr int kOriReps = 4;
 constexpr int kDescReps = 4;
 constexpr int kDescRepStride = 130;  // doubles; the pad rotates LDS banks
@@ -1421,11 +1472,11 @@ __device__ void describe(DescLdsT<MODE>& S, const PyrTable* __restrict__ pt, con
                 const float cb = col_rot + (float)(kDescW / 2 - 0.5);
                 const float dx = (float)(cv[0] - cv[1]);
                 const float dy = (float)(cv[2] - cv[3]);
-                const float mag = __builtin_sqrtf(fmaf(dx, dx, dy * dy));
+                const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));  // 1 ulp
                 // unwrapped angle: floor/fraction of the bin position are the
                 // reference's after wrapping into [0, 2pi); the bin index is
                 // reduced mod 8 instead (fmods of sift.cpp:667)
-                const float ob = (atan2f(dy, dx) - porif) * (float)(kDescBins / kTwoPi);
+                const float ob = (atan2_f32(dy, dx) - porif) * (float)(kDescBins / kTwoPi);
                 const float wgt =
                     __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
                 const float m = mag * wgt;

@@ -149,6 +149,7 @@ class RecordExchange:
         self.total = 0       # records pushed into it (true count)
         self.entries = []    # (image id, count)
         self.n_steps = 0     # steps in the current slot
+        self.staged = None   # "host" (push) or "device" (push_device)
 
     def _wait_slot(self, s: int) -> None:
         if self.done[s] is not None:
@@ -180,9 +181,14 @@ class RecordExchange:
             self._wait_slot(s)
             self.cur = s
             self._reset_fill()
-            if not self.cuda:  # unused checksum words of a short bucket read as 0
-                self.host[s].view(-1)[self.sum_word * 8:self.hdr_words * 8] = 0
+            # (host-staged) unused checksum words of a short bucket read as 0
+            self.host[s].view(-1)[self.sum_word * 8:self.hdr_words * 8] = 0
         return self.cur
+
+    def _stage(self, how: str) -> None:
+        if self.staged not in (None, how):
+            raise ValueError("push and push_device cannot share a bucket of steps")
+        self.staged = how
 
     def _header(self) -> torch.Tensor:
         """The host-built header words (before the per-step checksums)."""
@@ -216,7 +222,11 @@ class RecordExchange:
         hdr = self._header()
         h = self.host[s]
         h.view(-1)[: hdr.numel()] = hdr
-        n_host_bytes = hdr.numel() if self.cuda else (self.hdr_rows + self.fill) * RECORD_BYTES
+        # host-staged slots (push) go up whole: header, per-step checksums
+        # and records; device-filled ones (push_device) only the header words
+        # before the checksums, which the library wrote on the device
+        n_host_bytes = (hdr.numel() if self.staged == "device"
+                        else (self.hdr_rows + self.fill) * RECORD_BYTES)
         if self.cuda:
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.stream):
@@ -247,6 +257,7 @@ class RecordExchange:
         """Add this step's buffers (uint8 [n_i, 168], host) to the exchange;
         returns the slot index whose `gathered` buffer will hold the result."""
         s = self._open_slot()
+        self._stage("host")
         h = self.host[s]
         k = self.n_steps
         self._add_entries([int(t.shape[0]) for t in local], image_ids)
@@ -270,6 +281,7 @@ class RecordExchange:
         counts = sift_ctx.wait(ticket)
         n_rows = sum(counts)
         s = self._open_slot()
+        self._stage("device")
         k = self.n_steps
         base = self.dev[s][self.hdr_rows + self.fill:]
         room = self.cap - self.fill
@@ -295,7 +307,7 @@ class RecordExchange:
         """Start the collective of a partly filled bucket, then wait for
         every exchange in flight."""
         if self.cur is not None and self.n_steps > 0:
-            if self.cuda:  # checksum words of the bucket's missing steps
+            if self.staged == "device":  # checksum words of the missing steps
                 self.dev[self.cur].view(-1)[(self.sum_word + self.n_steps) * 8:
                                             self.hdr_words * 8].zero_()
             self._launch()

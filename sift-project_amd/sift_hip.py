@@ -352,13 +352,14 @@ class Context:
         return counts
 
     def verify_slots(self, slots_ptr: int, n_slots: int, slot_bytes: int, hdr_rows: int,
-                     count_word: int, sum_word: int, cap_rows: int, bad_ptr: int,
-                     stream: int = 0) -> None:
+                     count_word: int, sum_word: int, n_sum_words: int, cap_rows: int,
+                     bad_ptr: int, stream: int = 0) -> None:
         """Enqueue the exchange check of n_slots record slots (see
         include/sift_hip.h sift_hip_verify_slots)."""
         _check(self.lib.sift_hip_verify_slots(
             self._ctx, ctypes.c_void_p(slots_ptr), n_slots, slot_bytes, hdr_rows, count_word,
-            sum_word, cap_rows, ctypes.c_void_p(bad_ptr), ctypes.c_void_p(stream or None)))
+            sum_word, n_sum_words, cap_rows, ctypes.c_void_p(bad_ptr),
+            ctypes.c_void_p(stream or None)))
 
     def detect(self, img: np.ndarray, params: SiftParams | None = None, desc_f32: bool = False):
         """detect_keypoints_and_descriptors on a host image (H,W[,C] float64)."""

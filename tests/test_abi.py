@@ -115,3 +115,18 @@ def test_host_u8_packing_pass():
                 b = img.copy()
                 b[pos] = bad
                 assert not f(b.ctypes.data, n, out.ctypes.data), (n, bad, pos)
+
+
+def test_python_binding_argument_counts_match_the_header():
+    """Every argtypes list set by load_library has as many entries as the
+    header's declaration has parameters (a wrong count corrupts the call)."""
+    lib = load_library()
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for name in EXPORTS:
+        m = re.search(r"\b" + name + r"\s*\(([^)]*)\)", src)
+        if not m:
+            continue
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        fn = getattr(lib, name)
+        if fn.argtypes is not None:
+            assert len(fn.argtypes) == len(params), name
