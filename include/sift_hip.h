@@ -321,7 +321,9 @@ int sift_hip_copy_records_device(sift_ctx* ctx, void* d_dst, size_t cap,
 /* Host-side wall time (ms) of the phases of the last detect: [0] plan +
  * enqueue of every kernel, [1] wait for the device pipeline, [2] download of
  * the keypoint records, [3] final size + clean_keypoints, [4] output
- * assembly. Writes min(n, 5) values. */
+ * assembly, [5] the part of [1]-[3] the host spent blocked on device
+ * events (the rest is host work: per-chain sizes and sorted runs, merge).
+ * Writes min(n, 6) values. */
 int sift_hip_last_timing(sift_ctx* ctx, double* ms, int n);
 
 /* The context's HIP stream (hipStream_t), for event timing. */

@@ -226,7 +226,7 @@ struct Slot {
     bool gather_pending = false;
     sift_counts counts{};
     clk::time_point t_submit;
-    double t_host[5] = {0, 0, 0, 0, 0};
+    double t_host[6] = {0, 0, 0, 0, 0, 0};  // [5]: blocked on device events in finalize
 };
 
 }  // namespace
@@ -731,8 +731,15 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     s.n_keys = 0;
     s.run_start.clear();
     s.fin_ws.all.resize(s.exp_rec.cap);
+    double blocked = 0.0;  // host time spent waiting for the device
+    auto sync_ev = [&](hipEvent_t e) -> hipError_t {
+        const auto a = clk::now();
+        const hipError_t r = hipEventSynchronize(e);
+        blocked += ms(a, clk::now());
+        return r;
+    };
     for (int ci = 0; ci < s.n_chains; ++ci) {
-        SIFT_HIP_TRY(hipEventSynchronize(s.chain_ev[ci]));
+        SIFT_HIP_TRY(sync_ev(s.chain_ev[ci]));
         const unsigned b = s.exp_cnt.h[2 * ci], e = s.exp_cnt.h[2 * ci + 1];
         if (e > s.exp_lane || b > e) {
             s.exported = false;
@@ -788,7 +795,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
                                         hipMemcpyDeviceToHost, sC));
             SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
         }
-        SIFT_HIP_TRY(hipEventSynchronize(s.done_ev));
+        SIFT_HIP_TRY(sync_ev(s.done_ev));
         t_wait = clk::now();
         size_t nc = 0, nr = 0, no = 0;  // largest per-lane counts
         for (int L = 0; L < kLanes; ++L) {
@@ -849,7 +856,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     }
     if (bulk || s.want_df) {
         SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
-        SIFT_HIP_TRY(hipEventSynchronize(s.done_ev));
+        SIFT_HIP_TRY(sync_ev(s.done_ev));
     }
     const auto t_copy = clk::now();
 
@@ -887,6 +894,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     s.t_host[1] = ms(t0, t_wait);
     s.t_host[2] = ms(t_wait, t_copy);
     s.t_host[3] = ms(t_copy, t_fin);
+    s.t_host[5] = blocked;
 
     s.counts.extrema = (int64_t)s.lane_n[0][0] + s.lane_n[0][1];
     s.counts.refined = (int64_t)s.lane_n[1][0] + s.lane_n[1][1];
@@ -935,14 +943,20 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
         sift_params_default(&def);
         p = &def;
     }
+    // the lowest free slot that is not the introspected one (the last
+    // finalised job, sift_hip_copy_level & co.), else that one: a stream of
+    // jobs with d in flight cycles through d + 1 slots, whose grow-only
+    // buffers are then all warm (a rotation over every slot met cold,
+    // allocating slots for the first kSlots jobs)
     Slot* sp = nullptr;
-    for (int k = 0; k < kSlots; ++k) {  // a free slot, preferring not the introspected one
-        Slot& s = ctx->slots[(ctx->last + 1 + k + kSlots) % kSlots];
-        if (s.state == kFree) {
+    for (int k = 0; k < kSlots; ++k) {
+        Slot& s = ctx->slots[k];
+        if (s.state == kFree && k != ctx->last) {
             sp = &s;
             break;
         }
     }
+    if (!sp && ctx->last >= 0 && ctx->slots[ctx->last].state == kFree) sp = &ctx->slots[ctx->last];
     if (!sp) return SIFT_ERR_STATE;  // SIFT_MAX_INFLIGHT jobs already in flight
     Slot& s = *sp;
     if (s.gather_pending) {  // an async device fetch may still read its records
@@ -1514,7 +1528,7 @@ int sift_hip_last_timing(sift_ctx* ctx, double* ms, int n) {
     if (!ctx || !ms || n < 0) return SIFT_ERR_ARG;
     Slot* s = last_slot(ctx);
     if (!s) return SIFT_ERR_STATE;
-    for (int i = 0; i < n && i < 5; ++i) ms[i] = s->t_host[i];
+    for (int i = 0; i < n && i < 6; ++i) ms[i] = s->t_host[i];
     return SIFT_OK;
 }
 

@@ -33,6 +33,9 @@
 #ifndef SIFT_DESC_OCC
 #define SIFT_DESC_OCC 5  // k_descriptor (f32 math): min workgroups per CU
 #endif
+#ifndef SIFT_DESC_REPS
+#define SIFT_DESC_REPS 4  // k_descriptor: f64 histogram replicas per wave
+#endif
 #ifndef SIFT_EXT_PF
 #define SIFT_EXT_PF 2  // k_extrema_stream: rows in flight
 #endif
@@ -1285,7 +1288,7 @@ __device__ __forceinline__ float atan2_f32(float y, float x) {
 }
 
 constexpr int kOriReps = 4;
-constexpr int kDescReps = 4;
+constexpr int kDescReps = SIFT_DESC_REPS;  // f64 histogram replicas per wave (power of 2)
 constexpr int kDescRepStride = 130;  // doubles; the pad rotates LDS banks
 // k_orient: the replicas (4 * kOriReps * (num_bins + 2) doubles) and the
 // Gaussian weight table (kOriTab doubles) live in dynamic LDS sized per

@@ -515,9 +515,10 @@ class Context:
 
     def host_timing(self) -> dict:
         """Host-side phase wall times (ms) of the last detect."""
-        t = (ctypes.c_double * 5)()
-        _check(self.lib.sift_hip_last_timing(self._ctx, t, 5))
-        return dict(zip(("enqueue", "wait_device", "download", "finalize", "output"), list(t)))
+        t = (ctypes.c_double * 6)()
+        _check(self.lib.sift_hip_last_timing(self._ctx, t, 6))
+        return dict(zip(("enqueue", "wait_device", "download", "finalize", "output", "blocked"),
+                        list(t)))
 
     @property
     def stream(self) -> int:
