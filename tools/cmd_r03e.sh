@@ -3,4 +3,4 @@ export AB2_ARGS="--rounds 4 --steps 100 SIFT_SERIAL=1,DEPTH=1 SIFT_SERIAL=1,DEPT
 O=gpurun_out/r03e
 bash tools/gpu_session.sh r03e test ab ab2 bench || exit 1
 bash tools/pmc_kp.sh r03e/sq > $O/sq.log 2>&1 || { tail -5 $O/sq.log; exit 1; }
-python3 tools/sq_summary.py $O/sq/pass1/run_counter_collection.csv $O/sq/pass2/run_counter_collection.csv > $O/sq_summary.txt && cat $O/sq_summary.txt
+python3 tools/sq_summary.py $(ls $O/sq/pass1/*counter_collection.csv $O/sq/pass2/*counter_collection.csv) > $O/sq_summary.txt && cat $O/sq_summary.txt
