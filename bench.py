@@ -252,6 +252,7 @@ def host_busy_leg(ctx, ptrs, W, H, params, n_steps: int, depth: int) -> dict:
     step. If their sum approaches ms_per_step the loop is host-bound."""
     q = collections.deque()
     t_sub = t_fetch = t_wait = 0.0
+    ph = collections.Counter()
     t0 = time.perf_counter()
     for k in range(n_steps):
         while len(q) < depth and k + len(q) < n_steps:
@@ -261,14 +262,21 @@ def host_busy_leg(ctx, ptrs, W, H, params, n_steps: int, depth: int) -> dict:
         a = time.perf_counter()
         ctx.fetch(q.popleft())
         t_fetch += time.perf_counter() - a
-        t_wait += ctx.host_timing()["blocked"] * 1e-3
+        ht = ctx.host_timing()
+        t_wait += ht["blocked"] * 1e-3
+        ph.update({"enqueue": ht["enqueue"], "chain_runs": ht["wait_device"] - ht["blocked"],
+                   "merge_unique": ht["finalize"], "output_copy": ht["output"]})
     wall = time.perf_counter() - t0
     per = lambda x: x / n_steps * 1e3  # noqa: E731
     return {"ms_per_step": per(wall), "submit_ms": per(t_sub),
             "fetch_minus_device_wait_ms": per(t_fetch - t_wait),
             "host_busy_ms": per(t_sub + t_fetch - t_wait), "steps": n_steps,
+            "library_phases_ms": {k: v / n_steps for k, v in ph.items()},
             "note": "pipelined loop as the timed region; host_busy = submit + fetch - the "
-                    "time the library was blocked on device events"}
+                    "time the library was blocked on device events; library_phases_ms: "
+                    "enqueue (launches), chain_runs (glibc sizes + sorted run per keypoint "
+                    "chain while waiting), merge_unique, output_copy (records into the "
+                    "caller's array)"}
 
 
 def pipelined(ctx, submit, n_steps: int, depth: int = 0):

@@ -238,6 +238,9 @@ struct sift_ctx {
     // per CU; with two keypoint lanes in flight this leaves room for the
     // small octaves' blurs); measured best of 256/384/512/768/1024
     unsigned kp_wgs = 512;
+    // workgroups of the wavefront-per-record descriptor (4 records in flight
+    // each); SIFT_DESC_WGS
+    unsigned desc_wgs = 512;
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
     // rest form one final batch after the LDS octaves. A single-image job
     // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
@@ -257,7 +260,7 @@ struct sift_ctx {
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
     bool job_pairs = false;       // SIFT_JOB_STREAMS=2: two streams per job beyond the first
-    int desc_mode = 1;            // SIFT_DESC_MODE: k_descriptor variant (0 f64, 1 f32 math, 2 f32 hist)
+    int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
     int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
     // two stream pairs, one per hardware queue each (HIP's default is four
@@ -635,7 +638,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
                                    cap_ori, work, ctx->kp_wgs, sx));
         SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
-                                       work + 2, ex, ctx->kp_wgs, ctx->desc_mode, sx));
+                                       work + 2, ex, ctx->desc_mode == 1 ? ctx->desc_wgs : ctx->kp_wgs,
+                                       ctx->desc_mode, sx));
         SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], sx));
         return SIFT_OK;
     };
@@ -746,7 +750,6 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
             break;
         }
         const size_t base = (size_t)s.chain_lane[ci] * s.exp_lane;
-        host_sizes(p, s.exp_rec.h, s.exp_side.h, base + b, base + e);
         s.run_start.push_back(s.n_keys);
         host_sort_run(s.exp_rec.h, s.exp_side.h, (unsigned)(base + b), (unsigned)(base + e),
                       s.fin_ws.all.data() + s.n_keys, &s.fin_ws);
@@ -790,7 +793,8 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
                                        s.side.p, live + 2, cap_ori, work, ctx->kp_wgs, sC));
             SIFT_HIP_TRY(launch_descriptor(d_pt, s.dp, s.ori.p, s.side.p, zeros, live + 2, cap_ori,
                                            s.want_df ? s.df32.p : nullptr, work + 2, ex,
-                                           ctx->kp_wgs, ctx->desc_mode, sC));
+                                           ctx->desc_mode == 1 ? ctx->desc_wgs : ctx->kp_wgs,
+                                           ctx->desc_mode, sC));
             SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
             SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
@@ -1123,6 +1127,8 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
     if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::atoi(e);
     if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
+    if (const char* e = std::getenv("SIFT_DESC_WGS")) ctx->desc_wgs = (unsigned)std::atoi(e);
+    if (ctx->desc_wgs < 1) ctx->desc_wgs = 1;
     if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2"))
         ctx->batch_px_log2 = ctx->batch_px_log2_alone = std::atoi(e);
     if (const char* e = std::getenv("SIFT_KP_LANES")) ctx->lanes = std::atoi(e) == 1 ? 1 : kLanes;

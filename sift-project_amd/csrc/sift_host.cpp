@@ -110,18 +110,6 @@ int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* 
     return SIFT_OK;
 }
 
-void host_sizes(const sift_params* p, sift_kp* recs, const RecSide* side, size_t b, size_t e) {
-    for (size_t i = b; i < e; ++i) {
-        sift_kp& r = recs[i];
-        // std::pow(2, octave) is exactly 2^octave; ldexp gives the same value
-        const double scale = std::ldexp(1.0, r.octave);
-        double size = p->init_sigma * scale *
-                      std::pow(2, (static_cast<double>(r.layer) + side[i].off0) / p->intervals);
-        if (p->double_image_size) size /= 2;
-        r.size = size;
-    }
-}
-
 namespace {
 
 // image, then Keypoint::operator< (sift.hh:31-41): x asc, y asc, size desc,
@@ -227,7 +215,6 @@ size_t host_merge_unique(FinalizeKey* keys, const std::vector<unsigned>& run_sta
 
 size_t host_finalize(const sift_params* p, sift_kp* recs, const RecSide* side, unsigned n,
                      unsigned* keep, size_t* per_img, FinalizeWorkspace* ws) {
-    host_sizes(p, recs, side, 0, n);
     ws->all.resize(n);
     host_sort_run(recs, side, 0, n, ws->all.data(), ws);
     return host_merge_unique(ws->all.data(), {0u, n}, keep, per_img, ws);

@@ -29,10 +29,6 @@ struct Geometry {
 int host_plan(const sift_params* p, int w, int h, int c, Geometry* g, BlurTaps* taps_init,
               BlurTaps* taps, DevParams* dp);
 
-// Final keypoint size with glibc pow (sift.cpp:427-429, halved at
-// sift.cpp:525) written into recs[i].size for i in [b, e).
-void host_sizes(const sift_params* p, sift_kp* recs, const RecSide* side, size_t b, size_t e);
-
 // clean_keypoints (sift.cpp:20-24) in pieces, so a detect can sort the
 // records of each keypoint batch while the device still works on the next:
 // host_sort_run sorts the keys of records [b, e) into out[0, e-b) by image,
@@ -54,7 +50,8 @@ void host_sort_run(const sift_kp* recs, const RecSide* side, unsigned b, unsigne
                    FinalizeKey* out, FinalizeWorkspace* ws);
 size_t host_merge_unique(FinalizeKey* keys, const std::vector<unsigned>& run_start,
                          unsigned* keep, size_t* per_img, FinalizeWorkspace* ws);
-// all of it over records [0, n): sizes, one run, merge/unique
+// all of it over records [0, n): one run, merge/unique (the records carry
+// the device's glibc-exact size, sift_pow2.h)
 size_t host_finalize(const sift_params* p, sift_kp* recs, const RecSide* side, unsigned n,
                      unsigned* keep, size_t* per_img, FinalizeWorkspace* ws);
 

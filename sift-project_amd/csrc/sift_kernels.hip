@@ -1816,6 +1816,274 @@ __global__ __launch_bounds__(256, 4) void k_orient(
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_descriptor_wave (desc_mode 1, the default): one WAVEFRONT per record
+// (sift.cpp:610-682), four independent waves per workgroup pulling records
+// from the work counter; no workgroup barrier anywhere.
+//
+// Per-record cost was dominated by work every wave of the 256-thread
+// version repeated (record setup with f64 sin/cos, the f64 row-interval
+// solve with exact snapping, histogram zero/reduce/normalise): ~1150 VALU
+// instructions per wave per record against ~1100 for the samples
+// themselves (r02 SQ counters). Here a record's setup runs once, and:
+//  * The sample set is enumerated as an f32 SUPERSET of the reference's
+//    rotated box (row intervals widened by 0.01 column). No exact test is
+//    needed: a sample's trilinear weights vanish continuously at the box
+//    edges (row_bin -> -1 puts weight fr -> 0 on row 0 and the rest on the
+//    skipped row -1; row_bin -> 4 puts 1 - fr -> 0 on row 3), so a sample
+//    just outside contributes exactly nothing (its cells are skipped) and
+//    one just inside contributes ~1e-7 of its magnitude — the same order as
+//    the f32 sample math itself (contract: 1e-4 on the floats).
+//  * Sample math as describe<1> (f32, f64 histograms); the integer bounds
+//    (radius, image border) are exact.
+//  * kDescWReps lane-interleaved f64 replicas of the 4x4x8 histogram per
+//    wave; the 128 bins are reduced two per lane (bins l and l + 64), the
+//    two normalisation sums are in-wave reductions.
+// A wave's LDS instructions execute in order, so zeroing -> accumulation
+// -> reduction -> next record's zeroing needs only compiler ordering
+// (wave_sync).
+// ---------------------------------------------------------------------------
+#ifndef SIFT_DESCW_REPS
+#define SIFT_DESCW_REPS 4
+#endif
+#ifndef SIFT_DESCW_OCC
+#define SIFT_DESCW_OCC 5
+#endif
+#ifndef SIFT_DESCW_AHEAD
+#define SIFT_DESCW_AHEAD 1
+#endif
+constexpr int kDescWReps = SIFT_DESCW_REPS;
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
+    const PyrTable* __restrict__ pt, DevParams P, sift_kp* __restrict__ recs,
+    const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
+    const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
+    unsigned* __restrict__ work, ExportSink ex) {
+    __shared__ double hist_all[4 * kDescWReps * kDescRepStride];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double* const hist = hist_all + wv * kDescWReps * kDescRepStride;
+    double* const rep = hist + (lane & (kDescWReps - 1)) * kDescRepStride;
+    const unsigned n = min(*n_rec, cap_rec);
+    const unsigned k0 = min(*rec_begin, n);
+    // the launch's record range is fixed before it starts (orientation has
+    // completed); the host reads it after the chain's completion event
+    if (ex.cnt && blockIdx.x == 0 && threadIdx.x == 0) {
+        ex.cnt[0] = k0;
+        ex.cnt[1] = n;
+    }
+    constexpr float kHalfW = (float)(kDescW / 2 - 0.5);  // row_bin = row_rot + 1.5
+    const float wscale = (float)(-1.4426950408889634 / (0.5 * kDescW * kDescW));
+    for (;;) {
+        unsigned claim = 0;
+        if (lane == 0) claim = atomicAdd(work, 1u);
+        const unsigned k = k0 + __builtin_amdgcn_readfirstlane(claim);
+        if (k >= n) break;
+        // ---- record setup (wave-uniform)
+        const sift_kp& R = recs[k];
+        const double kx = R.x, ky = R.y, ksize = R.size, pori = R.pori;
+        const int o = R.octave, layer = R.layer;
+        const RecSide rside = rec_side[k];
+        gdouble* img = gbl(plane(pt, rside.img, o, layer));
+        const int W = pt->w[o], H = pt->h[o];
+        const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
+        const int x = (int)(kx * inv);
+        const int y = (int)(ky * inv);
+        const double hw = P.desc_scale_factor * (ksize * inv);
+        const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
+        const double diag = sqrt((double)(W * W + H * H));
+        const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
+        const int side = 2 * radius + 1;
+        float saf, caf;
+        sincosf((float)pori, &saf, &caf);
+        const float ihwf = (float)(1.0 / hw);
+        const float porif = (float)pori;
+        // |row_rot| < 2.5 and |col_rot| < 2.5, in units of hw
+        const float limf = (float)((0.5 * kDescW + 0.5) * hw);
+        for (int i = lane; i < kDescWReps * kDescRepStride; i += 64) hist[i] = 0.0;
+        wave_sync();
+        // ---- rows in groups of 64 (lane = row), samples 64 at a time
+        for (int g0 = 0; g0 < side; g0 += 64) {
+            const int row = g0 + lane - radius;
+            int lo = 0, len = 0;
+            if (g0 + lane < side && row + y > 0 && row + y < H - 1) {
+                const float fr = (float)row, ra = fr * caf, rs = fr * saf;
+                float clo = (float)max(-radius, 1 - x), chi = (float)min(radius, W - 2 - x);
+                // |c sa + r ca| < lim and |c ca - r sa| < lim, widened by 0.01
+                // column (f32 rounding of the bounds is far below that)
+                if (fabsf(saf) > 1e-6f) {
+                    const float is = 1.0f / saf;
+                    const float a1 = (-limf - ra) * is, a2 = (limf - ra) * is;
+                    clo = fmaxf(clo, fminf(a1, a2) - 0.01f);
+                    chi = fminf(chi, fmaxf(a1, a2) + 0.01f);
+                } else if (!(fabsf(ra) < limf + 0.01f)) {
+                    chi = clo - 1.0f;
+                }
+                if (fabsf(caf) > 1e-6f) {
+                    const float ic = 1.0f / caf;
+                    const float b1 = (-limf + rs) * ic, b2 = (limf + rs) * ic;
+                    clo = fmaxf(clo, fminf(b1, b2) - 0.01f);
+                    chi = fminf(chi, fmaxf(b1, b2) + 0.01f);
+                } else if (!(fabsf(rs) < limf + 0.01f)) {
+                    chi = clo - 1.0f;
+                }
+                lo = (int)ceilf(clo);
+                const int hi = (int)floorf(chi);
+                len = hi >= lo ? hi - lo + 1 : 0;
+            }
+            int pre = len;  // inclusive scan of the row lengths
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(pre, off);
+                if (lane >= off) pre += t;
+            }
+            const int total = __builtin_amdgcn_readlane(pre, 63);
+            int cur = 0;  // first row whose samples are not all consumed
+            // (row, col) of sample t0 + lane; false past the end
+            auto locate = [&](int t0, int& srow, int& scol) -> bool {
+                const int t = t0 + lane;
+                int r = cur, nxt = cur;
+                for (int q = cur; q < 64; ++q) {
+                    const int pq = __builtin_amdgcn_readlane(pre, q);
+                    if (pq > t0 + 63) break;
+                    r += (pq <= t) ? 1 : 0;
+                    nxt = q + 1;
+                }
+                const int lo_r = __shfl(lo, r);
+                const int ex_r = __shfl(pre, r) - __shfl(len, r);
+                cur = nxt;
+                srow = g0 + r - radius;
+                scol = lo_r + (t - ex_r);
+                return t < total;
+            };
+            // gradient loads issued unconditionally (see describe's fetch)
+            auto fetch = [&](bool ok, int srow, int scol, double* v) {
+                const size_t r0 = ok ? (size_t)(srow + y) * W + scol + x : (size_t)W + 1;
+                v[0] = img[r0 + 1];
+                v[1] = img[r0 - 1];
+                v[2] = img[r0 - W];
+                v[3] = img[r0 + W];
+            };
+            // kAhead blocks of 64 samples whose gradient loads are in flight
+            // while the current block is processed
+            constexpr int kAhead = SIFT_DESCW_AHEAD;
+            int srow = 0, scol = 0, qrow[kAhead], qcol[kAhead];
+            bool qok[kAhead];
+            double cv[4] = {0.0, 0.0, 0.0, 0.0}, qv[kAhead][4];
+            bool cok = total > 0 && locate(0, srow, scol);
+            fetch(cok, srow, scol, cv);
+#pragma unroll
+            for (int a = 0; a + 1 < kAhead; ++a) {
+                qrow[a] = qcol[a] = 0;
+                qok[a] = 64 * (a + 1) < total && locate(64 * (a + 1), qrow[a], qcol[a]);
+                fetch(qok[a], qrow[a], qcol[a], qv[a]);
+            }
+            for (int t0 = 0; t0 < total; t0 += 64) {
+                {
+                    int& nrow = qrow[kAhead - 1];
+                    int& ncol = qcol[kAhead - 1];
+                    nrow = ncol = 0;
+                    qok[kAhead - 1] =
+                        t0 + 64 * kAhead < total && locate(t0 + 64 * kAhead, nrow, ncol);
+                    fetch(qok[kAhead - 1], nrow, ncol, qv[kAhead - 1]);
+                }
+                if (cok) {
+                    const float fcol = (float)scol, frow = (float)srow;
+                    const float row_rot = fmaf(fcol, saf, frow * caf) * ihwf;
+                    const float col_rot = fmaf(fcol, caf, -(frow * saf)) * ihwf;
+                    const float rb = row_rot + kHalfW;
+                    const float cb = col_rot + kHalfW;
+                    const float dx = (float)(cv[0] - cv[1]);
+                    const float dy = (float)(cv[2] - cv[3]);
+                    const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
+                    const float ob = (atan2_f32(dy, dx) - porif) * (float)(kDescBins / kTwoPi);
+                    const float wgt =
+                        __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
+                    const float m = mag * wgt;
+                    const float fbr = floorf(rb), fbc = floorf(cb), fbo = floorf(ob);
+                    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
+                    const float fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
+#pragma unroll
+                    for (int rq = 0; rq <= 1; ++rq) {
+                        const int ri = br + rq;
+                        if ((unsigned)ri >= (unsigned)kDescW) continue;
+                        const float vr = m * ((rq == 0) ? 1.0f - fr : fr);
+#pragma unroll
+                        for (int cq = 0; cq <= 1; ++cq) {
+                            const int ci = bc + cq;
+                            if ((unsigned)ci >= (unsigned)kDescW) continue;
+                            const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
+                            double* hb = &rep[ri * 32 + ci * 8];
+                            atomicAdd(&hb[bo & 7], (double)(vc * (1.0f - fo)));
+                            atomicAdd(&hb[(bo + 1) & 7], (double)(vc * fo));
+                        }
+                    }
+                }
+                srow = qrow[0];
+                scol = qcol[0];
+                cok = qok[0];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cv[q] = qv[0][q];
+#pragma unroll
+                for (int a = 0; a + 1 < kAhead; ++a) {
+                    qrow[a] = qrow[a + 1];
+                    qcol[a] = qcol[a + 1];
+                    qok[a] = qok[a + 1];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
+                }
+            }
+        }
+        wave_sync();
+        // ---- reduce the replicas (bins lane, lane + 64), normalise, clamp,
+        // renormalise, quantise (sift.cpp:576-603)
+        double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+        for (int r = 0; r < kDescWReps; ++r) {
+            v0 += hist[r * kDescRepStride + lane];
+            v1 += hist[r * kDescRepStride + lane + 64];
+        }
+        const double ninv = 1.0 / sqrt(wave_sum_f64(v0 * v0 + v1 * v1));
+        double c0 = v0 * ninv, c1 = v1 * ninv;
+        if (c0 > kMagThr) c0 = kMagThr;
+        if (c1 > kMagThr) c1 = kMagThr;
+        const double inv2 = 1.0 / sqrt(wave_sum_f64(c0 * c0 + c1 * c1));
+        auto quant = [&](double c) -> uint8_t {
+            const double q = floor(kIntFactor * c * inv2);
+            int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
+            return (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
+        };
+        const uint8_t u0 = quant(c0), u1 = quant(c1);
+        recs[k].desc[lane] = u0;
+        recs[k].desc[lane + 64] = u1;
+        if (desc_f32) {
+            desc_f32[(size_t)k * 128 + lane] = (float)(c0 * inv2);
+            desc_f32[(size_t)k * 128 + lane + 64] = (float)(c1 * inv2);
+        }
+        if (k < ex.cap) {
+            ex.rec[k].desc[lane] = u0;
+            ex.rec[k].desc[lane + 64] = u1;
+            if (lane == 0) {
+                sift_kp& r = ex.rec[k];
+                r.x = kx;
+                r.y = ky;
+                r.octave = o;
+                r.layer = layer;
+                r.size = ksize;
+                r.pori = pori;
+                ex.side[k] = rside;
+            }
+        }
+        wave_sync();
+    }
+}
+
 // Descriptors of records [*rec_begin, *n_rec), one workgroup per record
 // from a work counter; workgroup 0 publishes the range.
 template <int MODE>
@@ -2242,8 +2510,15 @@ hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* 
                              unsigned* work, const ExportSink& ex, unsigned wgs,
                              int mode, hipStream_t s) {
     unsigned blocks = wgs;  // persistent: workgroups pull records
+    if (mode == 1) {  // four waves per workgroup, a record per wave
+        blocks = std::min<unsigned>(blocks, cap_rec > 0 ? (cap_rec + 3) / 4 : 1);
+        hipLaunchKernelGGL(k_descriptor_wave, dim3(blocks), dim3(256), 0, s, d_pt, P, recs,
+                           rec_side, rec_begin, n_rec, cap_rec, desc_f32, work, ex);
+        return hipGetLastError();
+    }
     if (blocks > cap_rec) blocks = cap_rec > 0 ? cap_rec : 1;
-    auto kern = mode == 0 ? k_descriptor<0> : mode == 1 ? k_descriptor<1> : k_descriptor<2>;
+    // 3: the 256-threads-per-record f32 variant (A/B against mode 1)
+    auto kern = mode == 0 ? k_descriptor<0> : mode == 3 ? k_descriptor<1> : k_descriptor<2>;
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_side,
                        rec_begin, n_rec, cap_rec, desc_f32, work, ex);
     return hipGetLastError();

@@ -272,14 +272,15 @@ def test_gpu_pyramid_paths_match_oracle(lds_px, shape):
 
 
 # Descriptor sample-math variants (SIFT_DESC_MODE): 0 = f64 sample math,
-# 1 = f32 sample math with f64 histograms (default), 2 = f32 histograms. Each
-# must meet the descriptor contract on the 1080p golden and on the
-# stb-decoded photographs (natural gradients).
+# 1 = wavefront per record, f32 superset enumeration and sample math with f64
+# histograms (default), 2 = f32 histograms, 3 = the 256-thread f32 variant
+# with exact f64 acceptance. Each must meet the descriptor contract on the
+# 1080p golden and on the stb-decoded photographs (natural gradients).
 DESC_GOLDENS = [g for g in GOLDENS if g.name in ("synth_1920x1080", "image1",
                                                  "photo_cave01_00")]
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("g", DESC_GOLDENS, ids=[g.name for g in DESC_GOLDENS])
 def test_gpu_descriptor_modes_match_golden(mode, g):
     import os
