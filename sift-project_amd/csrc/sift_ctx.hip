@@ -180,6 +180,7 @@ struct Slot {
     DevBuf<sift_kp> ori;
     DevBuf<RecSide> side;
     DevBuf<float> df32;
+    DevBuf<unsigned> lab;  // SIFT_LAB_DOUBLE: counters of the duplicate launches
     size_t cap_cand = 0, cap_raw = 0, cap_ori = 0;  // per lane
     unsigned* d_ctr = nullptr;
     unsigned* h_ctr = nullptr;  // pinned, live counters of every lane
@@ -234,13 +235,18 @@ struct Slot {
 struct sift_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // = pyr_stream[0]: the public stream (matcher)
-    // persistent workgroups of orientation / descriptor per launch: 512 (two
-    // per CU; with two keypoint lanes in flight this leaves room for the
-    // small octaves' blurs); measured best of 256/384/512/768/1024
-    unsigned kp_wgs = 512;
-    // workgroups of the wavefront-per-record descriptor (4 records in flight
-    // each); SIFT_DESC_WGS
-    unsigned desc_wgs = 512;
+    // persistent workgroups of orientation / descriptor per launch, per
+    // image of the job (capped at kp_wgs_max): four keypoints in flight per
+    // workgroup. Fewer than the chip could hold, deliberately: the keypoint
+    // kernels are gather-latency-bound, and in the pipelined steady state
+    // their resident waves take register file and memory bandwidth from the
+    // other jobs' blurs. Interleaved A/B on 1080p, single-image jobs (four in
+    // flight): 192 per image 0.521 ms, 256 0.527, 512 0.548; 8-image jobs
+    // want 512 in all (0.503 ms per image vs 0.537 at 1024, 0.516 at 768). SIFT_KP_WGS,
+    // SIFT_DESC_WGS, SIFT_KP_WGS_MAX
+    unsigned kp_wgs = 192;
+    unsigned desc_wgs = 192;
+    unsigned kp_wgs_max = 512;
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
     // rest form one final batch after the LDS octaves. A single-image job
     // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
@@ -257,9 +263,16 @@ struct sift_ctx {
     size_t lds_max_px = kLdsOctavePx;
     bool shared_streams = false;  // SIFT_SHARED_STREAMS=1: every job on all four streams
     bool serial = false;          // SIFT_SERIAL=1: every kernel on one stream (profiling)
+    // SIFT_LAB_DOUBLE (lab measurement only): every launch of the selected
+    // kernel families runs twice, the duplicate with its outputs discarded
+    // (capacity 0, scratch counters) or idempotent (blurs, descriptor bytes);
+    // the pipelined time difference is the family's marginal cost. Bits:
+    // 1 pyramid, 2 extrema, 4 refine, 8 orientation, 16 descriptor
+    unsigned lab_double = 0;
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
     bool job_pairs = false;       // SIFT_JOB_STREAMS=2: two streams per job beyond the first
+    int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
     int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
@@ -513,6 +526,9 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         double* tmp = wide ? s.tmp.p + (o & 1) * tmp_half : nullptr;
         SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp, so,
                                  e0, e1, ctx->tile_max_px));
+        if (ctx->lab_double & 1)
+            SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp,
+                                     so, nullptr, nullptr, ctx->tile_max_px));
         return SIFT_OK;
     };
 
@@ -633,13 +649,34 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 3));
         }
         const unsigned* b = begin ? begin : zeros;
+        const unsigned ori_wgs = std::min(ctx->kp_wgs_max, ctx->kp_wgs * (unsigned)n_img);
+        const unsigned desc_wgs = std::min(
+            ctx->kp_wgs_max, (ctx->desc_mode == 1 ? ctx->desc_wgs : ctx->kp_wgs) * (unsigned)n_img);
+        unsigned* lab = nullptr;  // 8 scratch counters of this chain's duplicates
+        if (ctx->lab_double & 30u) {
+            if ((st = s.lab.ensure(8 * (kMaxOctaves + 2))) != SIFT_OK) return st;
+            lab = s.lab.p + 8 * ci;
+            SIFT_HIP_TRY(hipMemsetAsync(lab, 0, 8 * sizeof(unsigned), sx));
+            if (ctx->lab_double & 2u)
+                SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
+                                                cand, lab, 0, nullptr, sx, nullptr, nullptr));
+        }
         SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
                                    raw, live + 1, cap_raw, sx));
+        if (ctx->lab_double & 4u)
+            SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0,
+                                       cap_cand, raw, lab + 1, 0, sx));
         SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
-                                   cap_ori, work, ctx->kp_wgs, sx));
+                                   cap_ori, work, ori_wgs, ctx->ori_mode, sx));
+        if (ctx->lab_double & 8u)
+            SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side,
+                                       lab + 2, 0, lab + 3, ori_wgs, ctx->ori_mode, sx));
         SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
-                                       work + 2, ex, ctx->desc_mode == 1 ? ctx->desc_wgs : ctx->kp_wgs,
-                                       ctx->desc_mode, sx));
+                                       work + 2, ex, desc_wgs, ctx->desc_mode, sx));
+        if (ctx->lab_double & 16u)
+            SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori,
+                                           nullptr, lab + 4, ExportSink{nullptr, nullptr, nullptr, 0},
+                                           desc_wgs, ctx->desc_mode, sx));
         SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], sx));
         return SIFT_OK;
     };
@@ -701,6 +738,9 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss, s.d_stage->taps,
                                         n_img, so, e0, e1));
+        if (ctx->lab_double & 1)
+            SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss,
+                                            s.d_stage->taps, n_img, so, nullptr, nullptr));
     }
     if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
     // lane D joins C, then the live counters come back on C: the job's last
@@ -790,10 +830,14 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
             SIFT_HIP_TRY(launch_refine(d_pt, s.dp, s.cand.p, zeros, live, cap_cand, s.raw.p,
                                        live + 1, cap_raw, sC));
             SIFT_HIP_TRY(launch_orient(d_pt, s.dp, s.raw.p, zeros, live + 1, cap_raw, s.ori.p,
-                                       s.side.p, live + 2, cap_ori, work, ctx->kp_wgs, sC));
+                                       s.side.p, live + 2, cap_ori, work,
+                                       std::min(ctx->kp_wgs_max, ctx->kp_wgs * s.n_img),
+                                       ctx->ori_mode, sC));
             SIFT_HIP_TRY(launch_descriptor(d_pt, s.dp, s.ori.p, s.side.p, zeros, live + 2, cap_ori,
                                            s.want_df ? s.df32.p : nullptr, work + 2, ex,
-                                           ctx->desc_mode == 1 ? ctx->desc_wgs : ctx->kp_wgs,
+                                           std::min(ctx->kp_wgs_max,
+                                                    (ctx->desc_mode == 1 ? ctx->desc_wgs
+                                                                         : ctx->kp_wgs) * s.n_img),
                                            ctx->desc_mode, sC));
             SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
@@ -1127,7 +1171,10 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
     if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::atoi(e);
     if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
+    if (const char* e = std::getenv("SIFT_KP_WGS_MAX")) ctx->kp_wgs_max = (unsigned)std::atoi(e);
+    if (ctx->kp_wgs_max < 1) ctx->kp_wgs_max = 1;
     if (const char* e = std::getenv("SIFT_DESC_WGS")) ctx->desc_wgs = (unsigned)std::atoi(e);
+    if (const char* e = std::getenv("SIFT_LAB_DOUBLE")) ctx->lab_double = (unsigned)std::atoi(e);
     if (ctx->desc_wgs < 1) ctx->desc_wgs = 1;
     if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2"))
         ctx->batch_px_log2 = ctx->batch_px_log2_alone = std::atoi(e);
@@ -1137,6 +1184,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_SHARED_STREAMS")) ctx->shared_streams = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
+    if (const char* e = std::getenv("SIFT_ORI_MODE")) ctx->ori_mode = std::atoi(e);
     if (const char* e = std::getenv("SIFT_JOB_STREAMS")) ctx->job_pairs = std::atoi(e) == 2;
     if (const char* e = std::getenv("SIFT_FUSE_INITIAL")) ctx->fuse_initial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
@@ -1193,6 +1241,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
         s.ori.release();
         s.side.release();
         s.df32.release();
+        s.lab.release();
         if (s.d_ctr) (void)hipFree(s.d_ctr);
         if (s.d_stage) (void)hipFree(s.d_stage);
         if (s.h_ctr) (void)hipHostFree(s.h_ctr);

@@ -1817,6 +1817,224 @@ __global__ __launch_bounds__(256, 4) void k_orient(
 }
 
 // ---------------------------------------------------------------------------
+// k_orient_wave (the default): compute_orientations (sift.cpp:447-533) with
+// one WAVEFRONT per refined keypoint, four independent waves per workgroup
+// pulling keypoints from the work counter; no workgroup barrier. Same
+// arithmetic as k_orient (f32 bin with the guarded exact f64 path, Gaussian
+// weights from a per-keypoint table of the same ocml exp, f64 replicas
+// summed in a fixed order, Gauss-Seidel smoothing in registers), but the
+// per-keypoint setup, table, smoothing and peak search run once per keypoint
+// instead of once per wave of a 256-thread workgroup. Per-wave dynamic LDS:
+// 4 replicas of num_bins + 2 doubles, the weight table (kOriWTab doubles),
+// and for num_bins > 64 the smoothed histogram.
+// ---------------------------------------------------------------------------
+#ifndef SIFT_ORIW_TAB
+#define SIFT_ORIW_TAB 512
+#endif
+constexpr int kOriWTab = SIFT_ORIW_TAB;
+
+__host__ __device__ constexpr int ori_wave_lds_doubles(int nb) {
+    return 4 * (nb + 2) + kOriWTab + (nb > 64 ? nb : 0);
+}
+
+__global__ __launch_bounds__(256, 4) void k_orient_wave(
+    const PyrTable* __restrict__ pt, DevParams P, const RawKp* __restrict__ raw,
+    const unsigned* __restrict__ raw_begin, const unsigned* __restrict__ n_raw, unsigned cap_raw,
+    sift_kp* __restrict__ recs, RecSide* __restrict__ rec_side, unsigned* __restrict__ n_rec,
+    unsigned cap_rec, unsigned* __restrict__ work) {
+    extern __shared__ double ori_wdyn[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned n = min(*n_raw, cap_raw);
+    const unsigned k0 = min(*raw_begin, n);
+    const int nb = P.num_bins;
+    const int stride = nb + 2;  // pad rotates LDS banks between replicas
+    double* const hist = ori_wdyn + wv * ori_wave_lds_doubles(nb);
+    double* const rep = hist + (lane & 3) * stride;
+    double* const wtab = hist + 4 * stride;
+    double* const hs = wtab + kOriWTab;  // num_bins > 64 only
+    const double bin_guard = nb * 3e-6;  // see k_orient
+    const float nbf = (float)nb;
+    for (;;) {
+        unsigned claim = 0;
+        if (lane == 0) claim = atomicAdd(work, 1u);
+        const unsigned k = k0 + __builtin_amdgcn_readfirstlane(claim);
+        if (k >= n) break;
+        const RawKp kp = raw[k];
+        const int o = kp.octave;
+        const double inv = 1.0 / pow2i(o);
+        const int x = (int)round(kp.x * inv);
+        const int y = (int)round(kp.y * inv);
+        const double scale = P.ori_sigma_factor * (kp.size * inv);
+        const int radius = (int)round(3.0 * scale);
+        const double denom = 2.0 * scale * scale;
+        gdouble* img = gbl(plane(pt, kp.img, o, kp.layer));
+        const int W = pt->w[o], H = pt->h[o];
+        const int side = 2 * radius + 1;
+        const int kmax = 2 * radius * radius;
+        const bool use_tab = kmax < kOriWTab;
+        for (int i = lane; i < 4 * stride; i += 64) hist[i] = 0.0;
+        if (use_tab)
+            for (int q = lane; q <= kmax; q += 64) wtab[q] = exp(-q / denom);
+        wave_sync();
+        // the side x side window flattened, 64 samples per step; sample s
+        // at (i, j) = (s % side, s / side) - radius
+        const int nsamp = side * side;
+        const int dj = 64 / side, di = 64 - dj * side;
+        int ci_ = lane % side - radius, cj_ = lane / side - radius;
+        auto advance = [&](int& i, int& j) {
+            i += di;
+            j += dj;
+            if (i > radius) {
+                i -= side;
+                ++j;
+            }
+        };
+        auto fetch = [&](int s, int i, int j, double* v) -> bool {
+            const bool ok =
+                !(s >= nsamp || x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H);
+            const size_t r0 = ok ? (size_t)(y + j) * W + x + i : (size_t)W + 1;
+            v[0] = img[r0 + 1];
+            v[1] = img[r0 - 1];
+            v[2] = img[r0 - W];
+            v[3] = img[r0 + W];
+            return ok;
+        };
+        double cv[4], nv[4];
+        bool cok = fetch(lane, ci_, cj_, cv);
+        int ni_ = ci_, nj_ = cj_;
+        advance(ni_, nj_);
+        for (int s0 = 0; s0 < nsamp; s0 += 64) {
+            const bool nok = fetch(s0 + 64 + lane, ni_, nj_, nv);
+            if (cok) {
+                const double dx = cv[0] - cv[1];
+                const double dy = cv[2] - cv[3];
+                const double mag = sqrt(dx * dx + dy * dy);
+                const int k2 = ci_ * ci_ + cj_ * cj_;
+                const double wgt = use_tab ? wtab[k2] : exp(-k2 / denom);
+                const float t = nbf * (atan2f((float)dy, (float)dx) + (float)kPi) *
+                                (float)(1.0 / kTwoPi);
+                int hidx = (int)rintf(t);
+                const bool tiny = (dx != 0.0 && fabs(dx) < 1e-30) || (dy != 0.0 && fabs(dy) < 1e-30);
+                if (fabs((double)t - floor((double)t) - 0.5) < bin_guard || tiny)
+                    hidx = (int)round(nb * (atan2(dy, dx) + kPi) / kTwoPi);  // exact path
+                hidx = (hidx < nb) ? hidx : 0;
+                atomicAdd(&rep[hidx], wgt * mag);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
+            cok = nok;
+            ci_ = ni_;
+            cj_ = nj_;
+            advance(ni_, nj_);
+        }
+        wave_sync();
+        // smoothing (sift.cpp:496-504) and peaks (sift.cpp:507-531)
+        double rx = kp.x, ry = kp.y, rs = kp.size;
+        if (P.double_image) {  // sift.cpp:522-526
+            rx /= 2;
+            ry /= 2;
+            rs /= 2;
+        }
+        auto emit = [&](bool peak, double ori) {  // one counter atomic per wave
+            const unsigned long long m = __ballot(peak);
+            if (!m) return;
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(n_rec, (unsigned)__popcll(m));
+            base = __builtin_amdgcn_readfirstlane(base);
+            const unsigned rec = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            if (peak && rec < cap_rec) {
+                sift_kp& r = recs[rec];
+                r.x = rx;
+                r.y = ry;
+                r.octave = kp.octave;
+                r.layer = kp.layer;
+                r.size = rs;
+                r.pori = ori;
+                rec_side[rec] = RecSide{kp.off0, kp.img, 0};
+            }
+        };
+        auto interp = [&](int i, double h0, double h1, double h2) {
+            double fi = i + 0.5 * (h0 - h2) / (h0 - 2 * h1 + h2);
+            fi = fmod(fi + nb, (double)nb);
+            double ori = kTwoPi * fi / nb;
+            return fmod(ori + kTwoPi, kTwoPi);
+        };
+        if (nb <= 64) {
+            // lane b holds bin b; the Gauss-Seidel chain runs through
+            // wave-uniform values, one dependent fma+add per bin (k_orient)
+            double h = 0.0;
+            if (lane < nb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) h += hist[r * stride + lane];
+            for (int it = 0; it < kSmoothIters; ++it) {
+                const double hn = __shfl(h, lane + 1 < nb ? lane + 1 : 0);  // old h[i+1]
+                const double c = 0.5 * h, d = 0.25 * hn;
+                double prev = readlane_f64(h, nb - 1);  // h[i-1] for i = 0: old
+                double first_new = 0.0, mine = h;
+                for (int i = 0; i < nb; ++i) {
+                    const double ci = readlane_f64(c, i);
+                    const double dn = (i + 1 == nb && i > 0) ? 0.25 * first_new : readlane_f64(d, i);
+                    const double v = fma(0.25, prev, ci) + dn;
+                    if (lane == i) mine = v;
+                    prev = v;
+                    if (i == 0) first_new = v;
+                }
+                h = mine;
+            }
+            double mx = lane < nb ? h : 0.0;  // bins >= 0
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+            const double h0 = __shfl(h, lane == 0 ? nb - 1 : lane - 1);
+            const double h2 = __shfl(h, lane + 1 >= nb ? 0 : lane + 1);
+            const bool peak = lane < nb && h > h0 && h > h2 && h > (P.peak_ratio * mx);
+            emit(peak, peak ? interp(lane, h0, h, h2) : 0.0);
+        } else {
+            for (int b = lane; b < nb; b += 64) {
+                double v = 0.0;
+                for (int r = 0; r < 4; ++r) v += hist[r * stride + b];
+                hs[b] = v;
+            }
+            wave_sync();
+            if (lane == 0) {
+                for (int it = 0; it < kSmoothIters; ++it) {
+                    double prev = hs[nb - 1];  // h[i-1] for i = 0: not yet updated
+                    const double h0_old = hs[0];
+                    double first_new = 0.0;
+                    for (int i = 0; i < nb; ++i) {
+                        const double h1 = hs[i];
+                        const double h2 = (i + 1 < nb) ? hs[i + 1] : (i == 0 ? h0_old : first_new);
+                        const double v = fma(0.25, prev, 0.5 * h1) + 0.25 * h2;
+                        hs[i] = v;
+                        prev = v;
+                        if (i == 0) first_new = v;
+                    }
+                }
+            }
+            wave_sync();
+            double mx = 0.0;
+            for (int b = lane; b < nb; b += 64) mx = fmax(mx, hs[b]);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+            for (int b0 = 0; b0 < nb; b0 += 64) {
+                const int i = b0 + lane;
+                bool peak = false;
+                double ori = 0.0;
+                if (i < nb) {
+                    const double h0 = hs[i == 0 ? nb - 1 : i - 1];
+                    const double h1 = hs[i];
+                    const double h2 = hs[i + 1 == nb ? 0 : i + 1];
+                    peak = h1 > h0 && h1 > h2 && h1 > (P.peak_ratio * mx);
+                    if (peak) ori = interp(i, h0, h1, h2);
+                }
+                emit(peak, ori);
+            }
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_descriptor_wave (desc_mode 1, the default): one WAVEFRONT per record
 // (sift.cpp:610-682), four independent waves per workgroup pulling records
 // from the work counter; no workgroup barrier anywhere.
@@ -2495,8 +2713,15 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
-                         unsigned* work, unsigned wgs, hipStream_t s) {
+                         unsigned* work, unsigned wgs, int mode, hipStream_t s) {
     unsigned blocks = wgs;  // persistent: workgroups pull keypoints
+    if (mode == 1) {  // four waves per workgroup, a keypoint per wave
+        blocks = std::min<unsigned>(blocks, cap_raw > 0 ? (cap_raw + 3) / 4 : 1);
+        const size_t lds = (size_t)4 * ori_wave_lds_doubles(P.num_bins) * sizeof(double);
+        hipLaunchKernelGGL(k_orient_wave, dim3(blocks), dim3(256), lds, s, d_pt, P, raw,
+                           raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work);
+        return hipGetLastError();
+    }
     if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
     const size_t lds = (size_t)(4 * kOriReps * (P.num_bins + 2) + kOriTab) * sizeof(double);
     hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), lds, s, d_pt, P, raw, raw_begin, n_raw,
