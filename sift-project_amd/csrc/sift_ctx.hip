@@ -204,6 +204,7 @@ struct Slot {
     // slot's pair)
     hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
     int lanes = kLanes;
+    int o_big = 0;  // octaves below: wavefront-per-keypoint kernels (enqueue_job)
     std::vector<EventPair> pending;
     // finalize
     bool exported = true;
@@ -247,6 +248,11 @@ struct sift_ctx {
     unsigned kp_wgs = 192;
     unsigned desc_wgs = 192;
     unsigned kp_wgs_max = 512;
+    unsigned kp_wgs_small = 512;   // SIFT_KP_WGS_SMALL: workgroup-per-keypoint chains
+    // octaves of fewer pixels per image use the workgroup-per-keypoint
+    // orientation / descriptor kernels (SIFT_KP_SMALL_PX; 0: never). Off:
+    // at 2^20 (1080p octaves >= 2) the extra chain cost 3.6 % pipelined
+    size_t kp_small_px = 0;
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
     // rest form one final batch after the LDS octaves. A single-image job
     // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
@@ -267,7 +273,8 @@ struct sift_ctx {
     // kernel families runs twice, the duplicate with its outputs discarded
     // (capacity 0, scratch counters) or idempotent (blurs, descriptor bytes);
     // the pipelined time difference is the family's marginal cost. Bits:
-    // 1 pyramid, 2 extrema, 4 refine, 8 orientation, 16 descriptor
+    // 1 strip blurs (planes > tile_max_px), 32 tile blurs, 64 LDS octaves,
+    // 2 extrema, 4 refine, 8 orientation, 16 descriptor
     unsigned lab_double = 0;
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
@@ -409,6 +416,93 @@ void abandon(sift_ctx* ctx, Slot& s) {
     s.ticket = -1;
 }
 
+// One keypoint chain: extrema over octaves [o_begin, o_end) -> refine ->
+// orientation -> descriptor, on lane `lane`'s arrays and live counters, on
+// stream sx. `begin` (the snapshot written by the extrema launch's last
+// workgroup) holds this chain's candidate end and its raw / record begins;
+// candidates start at cand_begin (the lane's previous chain's snapshot);
+// nullptr: the live counters (overflow re-run).
+struct ChainSpec {
+    int lane, o_begin, o_end;
+    const unsigned* cand_begin;
+    unsigned* begin;
+    hipStream_t sx;
+    unsigned* work;  // orientation / descriptor work counters (work, work + 2)
+    unsigned* lab;   // SIFT_LAB_DOUBLE: 8 scratch counters, or nullptr
+    ExportSink ex;
+};
+
+int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
+    const Geometry& g = s.g;
+    const DevParams& dp = s.dp;
+    const int n_img = s.n_img, L = c.lane, o_begin = c.o_begin, o_end = c.o_end;
+    const PyrTable* d_pt = &s.d_stage->pt;
+    const unsigned* zeros = s.d_ctr + kCtrZeros;
+    const unsigned cap_cand = (unsigned)s.cap_cand, cap_raw = (unsigned)s.cap_raw,
+                   cap_ori = (unsigned)s.cap_ori;
+    hipStream_t sx = c.sx;
+    unsigned* const begin = c.begin;
+    const unsigned* const cand_begin = c.cand_begin;
+    unsigned* const work = c.work;
+    unsigned* const lab = c.lab;
+    unsigned* live = s.d_ctr + 4 * L;
+    sift_extremum* cand = s.cand.p + (size_t)L * s.cap_cand;
+    RawKp* raw = s.raw.p + (size_t)L * s.cap_raw;
+    sift_kp* recs = s.ori.p + (size_t)L * s.cap_ori;
+    RecSide* side = s.side.p + (size_t)L * s.cap_ori;
+    float* df32 = s.want_df ? s.df32.p + (size_t)L * s.cap_ori * 128 : nullptr;
+    if (s.p.window_size / 2 == 1) {
+        // algorithmic bytes: every Gaussian level read once per pixel
+        double xb = 0.0;
+        for (int o = o_begin; o < o_end; ++o) xb += 8.0 * g.n_gauss * (double)g.W[o] * g.H[o];
+        hipEvent_t e0, e1;
+        if (prof_events(ctx, s, &e0, &e1, xb * n_img, SIFT_PROF_EXTREMA) != SIFT_OK)
+            return SIFT_ERR_HIP;
+        SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold, cand,
+                                        live + 0, cap_cand, begin, sx, e0, e1));
+    } else {
+        for (int o = o_begin; o < o_end; ++o)
+            SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], n_img, g.n_gauss,
+                                            s.p.window_size, dp.threshold, cand, live + 0,
+                                            cap_cand, sx));
+        if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 3));
+    }
+    const unsigned* b = begin ? begin : zeros;
+    // keypoint kernel flavour (octaves below o_big: wavefront per keypoint)
+    // and persistent grid of this chain (kp_wgs per image, also for a job
+    // alone on the chip: with 1024 workgroups the keypoint waves starved the
+    // concurrent small-octave blurs on the critical path, 1.03 vs 0.95 ms)
+    const bool small = o_begin >= s.o_big;
+    const int ori_mode = (small && ctx->ori_mode == 1) ? 0 : ctx->ori_mode;
+    const int desc_mode = (small && ctx->desc_mode == 1) ? 3 : ctx->desc_mode;
+    unsigned ori_wgs = std::min(ctx->kp_wgs_max, ctx->kp_wgs * (unsigned)n_img);
+    unsigned desc_wgs = std::min(ctx->kp_wgs_max, ctx->desc_wgs * (unsigned)n_img);
+    if (small) ori_wgs = desc_wgs = ctx->kp_wgs_small;
+    if (lab) {
+        SIFT_HIP_TRY(hipMemsetAsync(lab, 0, 8 * sizeof(unsigned), sx));
+        if (ctx->lab_double & 2u)
+            SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
+                                            cand, lab, 0, nullptr, sx, nullptr, nullptr));
+    }
+    SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
+                               raw, live + 1, cap_raw, sx));
+    if (lab && (ctx->lab_double & 4u))
+        SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0,
+                                   cap_cand, raw, lab + 1, 0, sx));
+    SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
+                               cap_ori, work, ori_wgs, ori_mode, sx));
+    if (lab && (ctx->lab_double & 8u))
+        SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, lab + 2,
+                                   0, lab + 3, ori_wgs, ori_mode, sx));
+    SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
+                                   work + 2, c.ex, desc_wgs, desc_mode, sx));
+    if (lab && (ctx->lab_double & 16u))
+        SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, nullptr,
+                                       lab + 4, ExportSink{nullptr, nullptr, nullptr, 0},
+                                       desc_wgs, desc_mode, sx));
+    return SIFT_OK;
+}
+
 // ---------------------------------------------------------------------------
 // enqueue one job on slot s (everything up to the counter read-back)
 // ---------------------------------------------------------------------------
@@ -418,7 +512,6 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     const Geometry& g = s.g;
     const int n_img = s.n_img;
     const sift_params* p = &s.p;
-    const DevParams& dp = s.dp;
     s.ev_i = 0;
     s.ev_used = 0;
     s.pending.clear();
@@ -526,7 +619,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         double* tmp = wide ? s.tmp.p + (o & 1) * tmp_half : nullptr;
         SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp, so,
                                  e0, e1, ctx->tile_max_px));
-        if (ctx->lab_double & 1)
+        if (ctx->lab_double & ((size_t)W * H > ctx->tile_max_px ? 1u : 32u))
             SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp,
                                      so, nullptr, nullptr, ctx->tile_max_px));
         return SIFT_OK;
@@ -574,7 +667,6 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             o_small = o;
             break;
         }
-    const bool tiles = p->window_size / 2 == 1;
     // Keypoint batches: each large octave (>= batch_px pixels over the job's
     // images) is its own batch as soon as its levels exist; the smaller ones,
     // whose keypoint work is too small to amortise a chain of launches, form
@@ -589,6 +681,23 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             break;
         }
     o_merge = std::min(o_merge, o_small);
+    // octaves [0, o_big) have at least kp_small_px pixels per image: their
+    // keypoints go through the wavefront-per-keypoint orientation /
+    // descriptor kernels, the smaller octaves' through the workgroup-per-
+    // keypoint ones (four waves per keypoint shorten the latency of each,
+    // which is what a launch over few keypoints is made of). A chain never
+    // mixes the two: the two flavours sum histograms in different orders, and
+    // a keypoint's records must not depend on how its job was batched. So
+    // octaves [o_merge, o_mid) form a chain of their own, enqueued after
+    // octave o_mid - 1, and the final chain starts at max(o_merge, o_mid).
+    // (kp_small_px 0, the default: every octave takes the wavefront kernels
+    // and there is no mid chain)
+    int o_big = 0;
+    while (o_big < g.octaves && (double)g.W[o_big] * g.H[o_big] >= (double)ctx->kp_small_px)
+        ++o_big;
+    if (o_big >= o_small) o_big = g.octaves;
+    const int o_mid = o_big == g.octaves ? o_merge : std::max(o_big, o_merge);
+    const int o_fin = o_mid;
     const unsigned* zeros = s.d_ctr + kCtrZeros;
     auto snap = [&](int gb) { return s.d_ctr + kCtrSnap + 4 * gb; };
     // records of every chain also go to the mapped export buffers, sized from
@@ -604,80 +713,29 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // lane L exports its records (lane-local index i) to exp_rec[L * exp_lane + i]
     s.exp_lane = s.exp_rec.cap / kLanes;
 
-    // extrema over [o_begin, o_end) then refine -> orientation -> descriptor,
-    // on lane L. `begin` (the snapshot written by the extrema launch's last
-    // workgroup) holds this batch's candidate end and its raw / record
-    // begins; candidates start at cand_begin (the lane's previous batch's
-    // snapshot). The overflow re-run passes nullptr (lane 0, live counters).
-    const unsigned cap_cand = (unsigned)s.cap_cand, cap_raw = (unsigned)s.cap_raw,
-                   cap_ori = (unsigned)s.cap_ori;
+    s.o_big = o_big;
     auto run_chain = [&](int L, int o_begin, int o_end, const unsigned* cand_begin,
                          unsigned* begin) -> int {
         const int ci = s.n_chains++;
         s.chain_lane.push_back(L);
-        hipStream_t sx = lane_stream[L];
-        unsigned* live = s.d_ctr + 4 * L;
-        sift_extremum* cand = s.cand.p + (size_t)L * s.cap_cand;
-        RawKp* raw = s.raw.p + (size_t)L * s.cap_raw;
-        sift_kp* recs = s.ori.p + (size_t)L * s.cap_ori;
-        RecSide* side = s.side.p + (size_t)L * s.cap_ori;
-        float* df32 = s.want_df ? s.df32.p + (size_t)L * s.cap_ori * 128 : nullptr;
-        unsigned* work = s.d_ctr + kCtrWork + 4 * ci;
         while ((int)s.chain_ev.size() <= ci) {
             hipEvent_t e;
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
                 return SIFT_ERR_HIP;
             s.chain_ev.push_back(e);
         }
-        const ExportSink ex{s.exp_rec.d + (size_t)L * s.exp_lane,
-                            s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
-                            (unsigned)s.exp_lane};
-        if (tiles) {
-            // algorithmic bytes: every Gaussian level read once per pixel
-            double xb = 0.0;
-            for (int o = o_begin; o < o_end; ++o) xb += 8.0 * g.n_gauss * (double)g.W[o] * g.H[o];
-            hipEvent_t e0, e1;
-            if (prof_events(ctx, s, &e0, &e1, xb * n_img, SIFT_PROF_EXTREMA) != SIFT_OK)
-                return SIFT_ERR_HIP;
-            SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
-                                            cand, live + 0, cap_cand, begin, sx, e0, e1));
-        } else {
-            for (int o = o_begin; o < o_end; ++o)
-                SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], n_img, g.n_gauss,
-                                                p->window_size, dp.threshold, cand, live + 0,
-                                                cap_cand, sx));
-            if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 3));
-        }
-        const unsigned* b = begin ? begin : zeros;
-        const unsigned ori_wgs = std::min(ctx->kp_wgs_max, ctx->kp_wgs * (unsigned)n_img);
-        const unsigned desc_wgs = std::min(
-            ctx->kp_wgs_max, (ctx->desc_mode == 1 ? ctx->desc_wgs : ctx->kp_wgs) * (unsigned)n_img);
         unsigned* lab = nullptr;  // 8 scratch counters of this chain's duplicates
         if (ctx->lab_double & 30u) {
             if ((st = s.lab.ensure(8 * (kMaxOctaves + 2))) != SIFT_OK) return st;
             lab = s.lab.p + 8 * ci;
-            SIFT_HIP_TRY(hipMemsetAsync(lab, 0, 8 * sizeof(unsigned), sx));
-            if (ctx->lab_double & 2u)
-                SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
-                                                cand, lab, 0, nullptr, sx, nullptr, nullptr));
         }
-        SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
-                                   raw, live + 1, cap_raw, sx));
-        if (ctx->lab_double & 4u)
-            SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0,
-                                       cap_cand, raw, lab + 1, 0, sx));
-        SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
-                                   cap_ori, work, ori_wgs, ctx->ori_mode, sx));
-        if (ctx->lab_double & 8u)
-            SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side,
-                                       lab + 2, 0, lab + 3, ori_wgs, ctx->ori_mode, sx));
-        SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
-                                       work + 2, ex, desc_wgs, ctx->desc_mode, sx));
-        if (ctx->lab_double & 16u)
-            SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori,
-                                           nullptr, lab + 4, ExportSink{nullptr, nullptr, nullptr, 0},
-                                           desc_wgs, ctx->desc_mode, sx));
-        SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], sx));
+        const ChainSpec c{L, o_begin, o_end, cand_begin, begin, lane_stream[L],
+                          s.d_ctr + kCtrWork + 4 * ci, lab,
+                          ExportSink{s.exp_rec.d + (size_t)L * s.exp_lane,
+                                     s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
+                                     (unsigned)s.exp_lane}};
+        if ((st = enqueue_chain(ctx, s, c)) != SIFT_OK) return st;
+        SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], c.sx));
         return SIFT_OK;
     };
     int n_batches = 0;
@@ -724,6 +782,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             }
         }
         if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
+        if (o + 1 == o_mid && o_merge < o_mid && (st = batch(o_merge, o_mid, {sA, sB})) != SIFT_OK)
+            return st;
     }
     if (o_small < g.octaves) {
         hipStream_t so = pyr[o_small & 1];
@@ -738,11 +798,11 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss, s.d_stage->taps,
                                         n_img, so, e0, e1));
-        if (ctx->lab_double & 1)
+        if (ctx->lab_double & 64u)
             SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss,
                                             s.d_stage->taps, n_img, so, nullptr, nullptr));
     }
-    if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
+    if (o_fin < g.octaves && (st = batch(o_fin, g.octaves, {sA, sB})) != SIFT_OK) return st;
     // lane D joins C, then the live counters come back on C: the job's last
     // device work (the final batch waited on both pyramid streams)
     if (sD != sC) {
@@ -801,44 +861,28 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     clk::time_point t_wait;
     for (int attempt = 0;; ++attempt) {
         if (attempt > 0) {
-            // the pyramid is complete: one chain over every octave, on C.
+            // the pyramid is complete: every octave again, on C.
             // Later jobs may be queued on the streams; they use other slots'
             // buffers, and the re-run simply queues behind them.
             s.exported = false;
             SIFT_HIP_TRY(hipMemsetAsync(s.d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
             s.n_chains = 0;
             s.chain_lane.clear();
-            // re-enqueue through the same code path with a single chain
-            const bool tiles = p->window_size / 2 == 1;
-            const PyrTable* d_pt = &s.d_stage->pt;
-            unsigned* live = s.d_ctr;
-            const unsigned* zeros = s.d_ctr + kCtrZeros;
-            unsigned* work = s.d_ctr + kCtrWork;
-            const unsigned cap_cand = (unsigned)s.cap_cand, cap_raw = (unsigned)s.cap_raw,
-                           cap_ori = (unsigned)s.cap_ori;
-            const ExportSink ex{s.exp_rec.d, s.exp_side.d, nullptr, 0};
-            if (tiles) {
-                SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, 0, g.octaves, s.n_img,
-                                                s.dp.threshold, s.cand.p, live, cap_cand, nullptr,
-                                                sC, nullptr, nullptr));
-            } else {
-                for (int o = 0; o < g.octaves; ++o)
-                    SIFT_HIP_TRY(launch_extrema_any(d_pt, o, g.W[o], g.H[o], s.n_img, g.n_gauss,
-                                                    p->window_size, s.dp.threshold, s.cand.p,
-                                                    live, cap_cand, sC));
+            // every octave again on lane 0, as two chains split at the kernel
+            // flavour boundary o_big (records as a normal run's); no export
+            const int ranges[3] = {0, std::min(s.o_big, g.octaves), g.octaves};
+            const unsigned* cb = s.d_ctr + kCtrZeros;
+            for (int r = 0; r < 2; ++r) {
+                if (ranges[r] >= ranges[r + 1]) continue;
+                unsigned* begin = s.d_ctr + kCtrSnap + 4 * s.n_chains;
+                const ChainSpec c{0, ranges[r], ranges[r + 1], cb, begin, sC,
+                                  s.d_ctr + kCtrWork + 4 * s.n_chains, nullptr,
+                                  ExportSink{s.exp_rec.d, s.exp_side.d, nullptr, 0}};
+                s.n_chains++;
+                s.chain_lane.push_back(0);
+                if ((st = enqueue_chain(ctx, s, c)) != SIFT_OK) return st;
+                cb = begin;
             }
-            SIFT_HIP_TRY(launch_refine(d_pt, s.dp, s.cand.p, zeros, live, cap_cand, s.raw.p,
-                                       live + 1, cap_raw, sC));
-            SIFT_HIP_TRY(launch_orient(d_pt, s.dp, s.raw.p, zeros, live + 1, cap_raw, s.ori.p,
-                                       s.side.p, live + 2, cap_ori, work,
-                                       std::min(ctx->kp_wgs_max, ctx->kp_wgs * s.n_img),
-                                       ctx->ori_mode, sC));
-            SIFT_HIP_TRY(launch_descriptor(d_pt, s.dp, s.ori.p, s.side.p, zeros, live + 2, cap_ori,
-                                           s.want_df ? s.df32.p : nullptr, work + 2, ex,
-                                           std::min(ctx->kp_wgs_max,
-                                                    (ctx->desc_mode == 1 ? ctx->desc_wgs
-                                                                         : ctx->kp_wgs) * s.n_img),
-                                           ctx->desc_mode, sC));
             SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
             SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
@@ -1173,6 +1217,8 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
     if (const char* e = std::getenv("SIFT_KP_WGS_MAX")) ctx->kp_wgs_max = (unsigned)std::atoi(e);
     if (ctx->kp_wgs_max < 1) ctx->kp_wgs_max = 1;
+    if (const char* e = std::getenv("SIFT_KP_WGS_SMALL")) ctx->kp_wgs_small = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_KP_SMALL_PX")) ctx->kp_small_px = (size_t)std::atoll(e);
     if (const char* e = std::getenv("SIFT_DESC_WGS")) ctx->desc_wgs = (unsigned)std::atoi(e);
     if (const char* e = std::getenv("SIFT_LAB_DOUBLE")) ctx->lab_double = (unsigned)std::atoi(e);
     if (ctx->desc_wgs < 1) ctx->desc_wgs = 1;

@@ -36,6 +36,21 @@
 #ifndef SIFT_DESC_REPS
 #define SIFT_DESC_REPS 4  // k_descriptor: f64 histogram replicas per wave
 #endif
+// wave issue priority (s_setprio) of the pyramid kernels, which share CUs
+// with the keypoint kernels' gather-bound waves (of their own job and of the
+// jobs in flight beside it): interleaved A/B, 1080p, single-image jobs four
+// in flight, priority 1 for all three -3.6 % over 20-step runs and -8.6 %
+// steady state; 3 for the LDS octaves and 2 for the tiles -3.5 / -6.3 %;
+// 8-image jobs +-1 %
+#ifndef SIFT_PRIO_STRIP
+#define SIFT_PRIO_STRIP 1
+#endif
+#ifndef SIFT_PRIO_TILE
+#define SIFT_PRIO_TILE 1
+#endif
+#ifndef SIFT_PRIO_LDS
+#define SIFT_PRIO_LDS 1
+#endif
 #ifndef SIFT_EXT_PF
 #define SIFT_EXT_PF 2  // k_extrema_stream: rows in flight
 #endif
@@ -193,6 +208,7 @@ template <int R, int C, bool DECIM, int MODE>
 __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict__ dst,
                                               size_t bs, int W, int H, int rows, BlurTaps taps,
                                               double* __restrict__ dec, int Wd, int Hd) {
+    if (SIFT_PRIO_STRIP > 0) __builtin_amdgcn_s_setprio(SIFT_PRIO_STRIP);
     constexpr int PF = SIFT_BLUR_PF;               // rows in flight ahead of the staged one
     constexpr int NW = 2 * R + 2;                  // register window depth
     constexpr int SPAN = 64 * C;                   // strip width
@@ -408,6 +424,7 @@ __global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ sr
                                                    double* __restrict__ dst, size_t bs, int W,
                                                    int H, BlurTaps taps,
                                                    double* __restrict__ dec, int Wd, int Hd) {
+    if (SIFT_PRIO_TILE > 0) __builtin_amdgcn_s_setprio(SIFT_PRIO_TILE);
     constexpr int SH = kTileH + 2 * R;             // staged rows
     constexpr int SWp = (kTileW + 2 * R) | 1;      // staged row stride (odd)
     constexpr int RX = 4, RY = 8;                  // output runs per task
@@ -649,6 +666,7 @@ __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
 __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
                                                       int o_first, int o_last, int n_gauss,
                                                       const BlurTaps* __restrict__ taps) {
+    if (SIFT_PRIO_LDS > 0) __builtin_amdgcn_s_setprio(SIFT_PRIO_LDS);
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, nt = blockDim.x;
     const int dec_level = n_gauss - 3;

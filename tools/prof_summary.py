@@ -36,8 +36,9 @@ def main(path, n_images=None):
         for r in seg:
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
             st = (int(r["Start_Timestamp"]) - t0) / 1000.0
-            print(f"  {r['Kernel_Name'][:30]:30s} start {st:8.1f} dur {d:8.1f} us  grid "
-                  f"{r['Grid_Size_X']}x{r['Grid_Size_Y']}")
+            q = r.get("Stream_Id") or r.get("Queue_Id") or "?"
+            print(f"  {r['Kernel_Name'][:30]:30s} start {st:8.1f} end {st + d:8.1f} dur {d:8.1f} us"
+                  f"  q {q:>3s} grid {r['Grid_Size_X']}x{r['Grid_Size_Y']}")
 
 
 if __name__ == "__main__":
