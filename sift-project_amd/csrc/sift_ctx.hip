@@ -280,14 +280,18 @@ struct sift_ctx {
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
     bool job_pairs = false;       // SIFT_JOB_STREAMS=2: two streams per job beyond the first
-    // SIFT_STREAM_POLICY 1 (default): a pipelined job takes one stream of the
-    // normal-priority pool, and a caller seen pipelining keeps that even when
-    // its pipeline is momentarily empty (pipe_hint). Interleaved A/B, 1080p,
-    // four in flight: -4 % over 20-step runs, -2.4 % steady state, 8-image
-    // jobs and synchronous latency unchanged (profiles/r03_e). 0: round 2's
-    // policy (a job alone takes all four pair streams, e.g. the first job of
-    // a burst, whose followers then share its hardware queues)
-    int stream_policy = 1;
+    // SIFT_STREAM_POLICY (A/B knob; default 0): 0 = a job alone takes all
+    // four pair streams, next to one other a free pair, else one free stream
+    // (pair streams first). 1 = pipelined jobs take one normal-priority
+    // stream each, and a caller seen pipelining keeps that when its pipeline
+    // is momentarily empty (pipe_hint); 2 = the same from the pair streams
+    // first. HIP gives each stream priority its own pool of at most
+    // GPU_MAX_HW_QUEUES hardware queues, shared by every stream of that
+    // priority in the process (torch's among them): policy 1 measured -4 %
+    // as the second context of an in-process A/B but +23 % as the bench's
+    // only context (0.72 vs 0.585 ms per step); policy 2 = policy 0 within
+    // noise (profiles/r03_e)
+    int stream_policy = 0;
     int pipe_hint = 0;
     int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
@@ -1090,14 +1094,14 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
         // to another in the last kPipeHint submits) gets one stream per job
         // even when its pipeline is momentarily empty, so the next jobs of a
         // burst find their hardware queues free (SIFT_STREAM_POLICY=1)
-        const bool hinted = ctx->stream_policy == 1 && ctx->pipe_hint > 0;
+        const bool hinted = ctx->stream_policy >= 1 && ctx->pipe_hint > 0;
         if (others > 0) ctx->pipe_hint = kPipeHint;
         else if (ctx->pipe_hint > 0) --ctx->pipe_hint;
-        if (ctx->stream_policy == 1 && (hinted || others > 0) && !ctx->shared_streams &&
+        if (ctx->stream_policy >= 1 && (hinted || others > 0) && !ctx->shared_streams &&
             !ctx->serial) {
-            // one stream of the normal-priority pool (kSlots - 4 of them),
-            // else any free one
-            int k = 2 * kPairs;
+            // one stream: policy 1 from the normal-priority pool first,
+            // policy 2 from the four pair streams first; else any free one
+            int k = ctx->stream_policy == 1 ? 2 * kPairs : 0;
             while (k < kSlots && (used >> k & 1u)) ++k;
             if (k == kSlots) {
                 k = 0;

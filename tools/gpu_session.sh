@@ -36,6 +36,8 @@ for step in "$@"; do
     python tools/prof_summary.py $O/ser/run_kernel_trace.csv > $O/summary_serial.txt
     cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv 2>/dev/null
     cp $O/ser/run_kernel_stats.csv $O/kernel_stats_serial.csv 2>/dev/null
+    # the traces themselves are tens of MB (gpurun copies back <= 64 MiB)
+    rm -rf $O/prof $O/ser
     echo PROF_DONE ;;
   ab|ab2|ab3)
     # interleaved A/B; variants and options from $AB_ARGS (resp. $AB2_ARGS, $AB3_ARGS)
