@@ -2089,6 +2089,10 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
 #define SIFT_DESCW_AHEAD 1
 #endif
 constexpr int kDescWReps = SIFT_DESCW_REPS;
+// replica stride (doubles): 129 = 258 dwords puts replica r's copy of a bin
+// 2r banks after replica 0's (ds_add_f64 serves 16 lanes per LDS cycle over
+// 32 banks), so 16 replicas = 16 distinct bank pairs for a bin
+constexpr int kDescWStride = kDescWReps >= 16 ? 129 : kDescRepStride;
 
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
@@ -2101,11 +2105,15 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
     const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
     const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
     unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ double hist_all[4 * kDescWReps * kDescRepStride];
+    __shared__ double hist_all[4 * kDescWReps * kDescWStride];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double* const hist = hist_all + wv * kDescWReps * kDescRepStride;
-    double* const rep = hist + (lane & (kDescWReps - 1)) * kDescRepStride;
+    double* const hist = hist_all + wv * kDescWReps * kDescWStride;
+#ifndef SIFT_LAB_REPHI
+    double* const rep = hist + (lane & (kDescWReps - 1)) * kDescWStride;
+#else  // lab: the 16 lanes of an LDS group share one replica
+    double* const rep = hist + ((lane >> 4) & (kDescWReps - 1)) * kDescWStride;
+#endif
     const unsigned n = min(*n_rec, cap_rec);
     const unsigned k0 = min(*rec_begin, n);
     // the launch's record range is fixed before it starts (orientation has
@@ -2142,7 +2150,7 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
         const float porif = (float)pori;
         // |row_rot| < 2.5 and |col_rot| < 2.5, in units of hw
         const float limf = (float)((0.5 * kDescW + 0.5) * hw);
-        for (int i = lane; i < kDescWReps * kDescRepStride; i += 64) hist[i] = 0.0;
+        for (int i = lane; i < kDescWReps * kDescWStride; i += 64) hist[i] = 0.0;
         wave_sync();
         // ---- rows in groups of 64 (lane = row), samples 64 at a time
         for (int g0 = 0; g0 < side; g0 += 64) {
@@ -2256,8 +2264,12 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
                             if ((unsigned)ci >= (unsigned)kDescW) continue;
                             const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
                             double* hb = &rep[ri * 32 + ci * 8];
+#ifndef SIFT_LAB_NOHIST
                             atomicAdd(&hb[bo & 7], (double)(vc * (1.0f - fo)));
                             atomicAdd(&hb[(bo + 1) & 7], (double)(vc * fo));
+#else
+                            if (vc == 12345.0f) hb[bo & 7] = fo;  // lab: no accumulation
+#endif
                         }
                     }
                 }
@@ -2282,8 +2294,8 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
         double v0 = 0.0, v1 = 0.0;
 #pragma unroll
         for (int r = 0; r < kDescWReps; ++r) {
-            v0 += hist[r * kDescRepStride + lane];
-            v1 += hist[r * kDescRepStride + lane + 64];
+            v0 += hist[r * kDescWStride + lane];
+            v1 += hist[r * kDescWStride + lane + 64];
         }
         const double ninv = 1.0 / sqrt(wave_sum_f64(v0 * v0 + v1 * v1));
         double c0 = v0 * ninv, c1 = v1 * ninv;
