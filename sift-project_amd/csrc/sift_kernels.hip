@@ -930,6 +930,16 @@ __device__ __forceinline__ double dpp_from_right(double v) {  // lane i <- lane 
     return __hiloint2double(hi, lo);
 }
 
+// level loads of the extrema scan: read once (SIFT_EXT_NT=1: non-temporal,
+// so they do not displace the lines other jobs' blurs re-read from L2/MALL)
+#ifndef SIFT_EXT_NT
+#define SIFT_EXT_NT 0
+#endif
+__device__ __forceinline__ double ext_load(gdouble* p) {
+    if (SIFT_EXT_NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
 template <int NL>
 __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restrict__ pt,
                                                         ExtremaGrid eg, int thr,
@@ -985,7 +995,7 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
         for (int p = 0; p < PF; ++p) {
             const size_t ro = (size_t)min(r0 + p, r1) * W;
 #pragma unroll
-            for (int l = 0; l < NL; ++l) pf[p][l] = lv[l][ro];
+            for (int l = 0; l < NL; ++l) pf[p][l] = ext_load(&lv[l][ro]);
         }
         double hmx[3][ND], hmn[3][ND], dc[3][NZ];
 #pragma unroll
@@ -1007,7 +1017,7 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
                     {
                         const size_t ro = (size_t)min(r + PF, r1) * W;
 #pragma unroll
-                        for (int l = 0; l < NL; ++l) pf[PF - 1][l] = lv[l][ro];
+                        for (int l = 0; l < NL; ++l) pf[PF - 1][l] = ext_load(&lv[l][ro]);
                     }
                     // row r: DoG, horizontal 3-max / 3-min per layer
 #pragma unroll
@@ -1843,16 +1853,25 @@ __global__ __launch_bounds__(256, 4) void k_orient(
 // summed in a fixed order, Gauss-Seidel smoothing in registers), but the
 // per-keypoint setup, table, smoothing and peak search run once per keypoint
 // instead of once per wave of a 256-thread workgroup. Per-wave dynamic LDS:
-// 4 replicas of num_bins + 2 doubles, the weight table (kOriWTab doubles),
-// and for num_bins > 64 the smoothed histogram.
+// 16 replica-interleaved copies of the histogram, the weight table
+// (kOriWTab doubles), and for num_bins > 64 the smoothed histogram.
 // ---------------------------------------------------------------------------
 #ifndef SIFT_ORIW_TAB
 #define SIFT_ORIW_TAB 512
 #endif
 constexpr int kOriWTab = SIFT_ORIW_TAB;
 
+// SIFT_ORIW_REPS replica-interleaved copies of the histogram per wave (bin b
+// of replica r at hist[b * reps + r], r = lane % reps). 16 make the atomics
+// conflict-free (see k_descriptor_wave) but the larger footprint measured
+// +2.3 % on the bench (8: +1 %) against 4 (profiles/r03_h/bench_ab.json)
+#ifndef SIFT_ORIW_REPS
+#define SIFT_ORIW_REPS 4
+#endif
+constexpr int kOriWReps = SIFT_ORIW_REPS;
+
 __host__ __device__ constexpr int ori_wave_lds_doubles(int nb) {
-    return 4 * (nb + 2) + kOriWTab + (nb > 64 ? nb : 0);
+    return kOriWReps * nb + kOriWTab + (nb > 64 ? nb : 0);
 }
 
 __global__ __launch_bounds__(256, 4) void k_orient_wave(
@@ -1866,10 +1885,9 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
     const unsigned n = min(*n_raw, cap_raw);
     const unsigned k0 = min(*raw_begin, n);
     const int nb = P.num_bins;
-    const int stride = nb + 2;  // pad rotates LDS banks between replicas
     double* const hist = ori_wdyn + wv * ori_wave_lds_doubles(nb);
-    double* const rep = hist + (lane & 3) * stride;
-    double* const wtab = hist + 4 * stride;
+    double* const rep = hist + (lane & (kOriWReps - 1));  // bin b at rep[b * kOriWReps]
+    double* const wtab = hist + kOriWReps * nb;
     double* const hs = wtab + kOriWTab;  // num_bins > 64 only
     const double bin_guard = nb * 3e-6;  // see k_orient
     const float nbf = (float)nb;
@@ -1891,7 +1909,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
         const int side = 2 * radius + 1;
         const int kmax = 2 * radius * radius;
         const bool use_tab = kmax < kOriWTab;
-        for (int i = lane; i < 4 * stride; i += 64) hist[i] = 0.0;
+        for (int i = lane; i < kOriWReps * nb; i += 64) hist[i] = 0.0;
         if (use_tab)
             for (int q = lane; q <= kmax; q += 64) wtab[q] = exp(-q / denom);
         wave_sync();
@@ -1937,7 +1955,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
                 if (fabs((double)t - floor((double)t) - 0.5) < bin_guard || tiny)
                     hidx = (int)round(nb * (atan2(dy, dx) + kPi) / kTwoPi);  // exact path
                 hidx = (hidx < nb) ? hidx : 0;
-                atomicAdd(&rep[hidx], wgt * mag);
+                atomicAdd(&rep[hidx * kOriWReps], wgt * mag);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) cv[q] = nv[q];
@@ -1982,9 +2000,10 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             // lane b holds bin b; the Gauss-Seidel chain runs through
             // wave-uniform values, one dependent fma+add per bin (k_orient)
             double h = 0.0;
-            if (lane < nb)
+            if (lane < nb)  // fixed order per bin, rotated by lane (banks)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) h += hist[r * stride + lane];
+                for (int q = 0; q < kOriWReps; ++q)
+                    h += hist[lane * kOriWReps + ((q + lane) & (kOriWReps - 1))];
             for (int it = 0; it < kSmoothIters; ++it) {
                 const double hn = __shfl(h, lane + 1 < nb ? lane + 1 : 0);  // old h[i+1]
                 const double c = 0.5 * h, d = 0.25 * hn;
@@ -2010,7 +2029,8 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
         } else {
             for (int b = lane; b < nb; b += 64) {
                 double v = 0.0;
-                for (int r = 0; r < 4; ++r) v += hist[r * stride + b];
+                for (int q = 0; q < kOriWReps; ++q)
+                    v += hist[b * kOriWReps + ((q + b) & (kOriWReps - 1))];
                 hs[b] = v;
             }
             wave_sync();
@@ -2072,28 +2092,36 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
 //    the f32 sample math itself (contract: 1e-4 on the floats).
 //  * Sample math as describe<1> (f32, f64 histograms); the integer bounds
 //    (radius, image border) are exact.
-//  * kDescWReps lane-interleaved f64 replicas of the 4x4x8 histogram per
+//  * kDescWReps replica-interleaved f64 copies of the 4x4x8 histogram per
 //    wave; the 128 bins are reduced two per lane (bins l and l + 64), the
 //    two normalisation sums are in-wave reductions.
 // A wave's LDS instructions execute in order, so zeroing -> accumulation
 // -> reduction -> next record's zeroing needs only compiler ordering
 // (wave_sync).
 // ---------------------------------------------------------------------------
-#ifndef SIFT_DESCW_REPS
-#define SIFT_DESCW_REPS 4
+#ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
+#define SIFT_DESCW_REPS 16
 #endif
-#ifndef SIFT_DESCW_OCC
-#define SIFT_DESCW_OCC 5
+#ifndef SIFT_DESCW_OCC  // min workgroups per CU (16 replicas: 64 KB LDS each)
+#define SIFT_DESCW_OCC (SIFT_DESCW_REPS >= 16 ? 2 : 5)
+#endif
+#ifndef SIFT_DESCW_WALK
+#define SIFT_DESCW_WALK 0
 #endif
 #ifndef SIFT_DESCW_AHEAD
 #define SIFT_DESCW_AHEAD 1
 #endif
 constexpr int kDescWReps = SIFT_DESCW_REPS;
-// replica stride (doubles): 129 = 258 dwords puts replica r's copy of a bin
-// 2r banks after replica 0's (ds_add_f64 serves 16 lanes per LDS cycle over
-// 32 banks), so 16 replicas = 16 distinct bank pairs for a bin
-constexpr int kDescWStride = kDescWReps >= 16 ? 129 : kDescRepStride;
-
+static_assert(kDescWReps >= 1 && kDescWReps <= 16 && (kDescWReps & (kDescWReps - 1)) == 0,
+              "replicas: a power of two <= 16");
+// Replica-interleaved layout: bin i of replica r at hist[i * kDescWReps + r],
+// r = lane % kDescWReps. ds_add_f64 serves 16 lanes per LDS cycle over 32
+// banks (bank = dword address mod 32); a lane's bank pair is then
+// 2 (i * kDescWReps + r) mod 32, so with 16 replicas every lane of a group
+// owns its bank pair whatever bins the samples hit (conflict-free), with 8
+// two lanes share a replica and collide only on bins of equal parity. (A
+// replica-major layout, r * stride + i, leaves the bank to the bin: the
+// atomics measured ~1 extra LDS cycle per LDS cycle, lane % 4 or % 16 alike.)
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
@@ -2105,15 +2133,11 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
     const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
     const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
     unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ double hist_all[4 * kDescWReps * kDescWStride];
+    __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kDescWReps];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double* const hist = hist_all + wv * kDescWReps * kDescWStride;
-#ifndef SIFT_LAB_REPHI
-    double* const rep = hist + (lane & (kDescWReps - 1)) * kDescWStride;
-#else  // lab: the 16 lanes of an LDS group share one replica
-    double* const rep = hist + ((lane >> 4) & (kDescWReps - 1)) * kDescWStride;
-#endif
+    double* const hist = hist_all + wv * 128 * kDescWReps;
+    double* const rep = hist + (lane & (kDescWReps - 1));  // bin i at rep[i * kDescWReps]
     const unsigned n = min(*n_rec, cap_rec);
     const unsigned k0 = min(*rec_begin, n);
     // the launch's record range is fixed before it starts (orientation has
@@ -2150,7 +2174,8 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
         const float porif = (float)pori;
         // |row_rot| < 2.5 and |col_rot| < 2.5, in units of hw
         const float limf = (float)((0.5 * kDescW + 0.5) * hw);
-        for (int i = lane; i < kDescWReps * kDescWStride; i += 64) hist[i] = 0.0;
+        for (int i = lane; i < 64 * kDescWReps; i += 64)
+            reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
         wave_sync();
         // ---- rows in groups of 64 (lane = row), samples 64 at a time
         for (int g0 = 0; g0 < side; g0 += 64) {
@@ -2188,10 +2213,16 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
                 if (lane >= off) pre += t;
             }
             const int total = __builtin_amdgcn_readlane(pre, 63);
-            int cur = 0;  // first row whose samples are not all consumed
-            // (row, col) of sample t0 + lane; false past the end
+            // (row, col) of sample t0 + lane; false past the end. Its row r
+            // is the number of rows whose inclusive prefix is <= t: a
+            // branch-free binary search over the 64 prefixes (the scalar
+            // walk over the rows a block touches cost ~20 SALU per block)
+#if SIFT_DESCW_WALK
+            int cur = 0;  // A/B: the scalar walk
+#endif
             auto locate = [&](int t0, int& srow, int& scol) -> bool {
                 const int t = t0 + lane;
+#if SIFT_DESCW_WALK
                 int r = cur, nxt = cur;
                 for (int q = cur; q < 64; ++q) {
                     const int pq = __builtin_amdgcn_readlane(pre, q);
@@ -2199,9 +2230,15 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
                     r += (pq <= t) ? 1 : 0;
                     nxt = q + 1;
                 }
+                cur = nxt;
+#else
+                int r = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (__shfl(pre, r + step - 1) <= t) r += step;
+#endif
                 const int lo_r = __shfl(lo, r);
                 const int ex_r = __shfl(pre, r) - __shfl(len, r);
-                cur = nxt;
                 srow = g0 + r - radius;
                 scol = lo_r + (t - ex_r);
                 return t < total;
@@ -2263,13 +2300,9 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
                             const int ci = bc + cq;
                             if ((unsigned)ci >= (unsigned)kDescW) continue;
                             const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
-                            double* hb = &rep[ri * 32 + ci * 8];
-#ifndef SIFT_LAB_NOHIST
-                            atomicAdd(&hb[bo & 7], (double)(vc * (1.0f - fo)));
-                            atomicAdd(&hb[(bo + 1) & 7], (double)(vc * fo));
-#else
-                            if (vc == 12345.0f) hb[bo & 7] = fo;  // lab: no accumulation
-#endif
+                            double* hb = &rep[(ri * 32 + ci * 8) * kDescWReps];
+                            atomicAdd(&hb[(bo & 7) * kDescWReps], (double)(vc * (1.0f - fo)));
+                            atomicAdd(&hb[((bo + 1) & 7) * kDescWReps], (double)(vc * fo));
                         }
                     }
                 }
@@ -2293,9 +2326,12 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
         // renormalise, quantise (sift.cpp:576-603)
         double v0 = 0.0, v1 = 0.0;
 #pragma unroll
-        for (int r = 0; r < kDescWReps; ++r) {
-            v0 += hist[r * kDescWStride + lane];
-            v1 += hist[r * kDescWStride + lane + 64];
+        for (int q = 0; q < kDescWReps; ++q) {
+            // fixed order per bin, rotated by lane so the 16 lanes of a read
+            // group start on different bank pairs
+            const int r = (q + lane) & (kDescWReps - 1);
+            v0 += hist[lane * kDescWReps + r];
+            v1 += hist[(lane + 64) * kDescWReps + r];
         }
         const double ninv = 1.0 / sqrt(wave_sum_f64(v0 * v0 + v1 * v1));
         double c0 = v0 * ninv, c1 = v1 * ninv;

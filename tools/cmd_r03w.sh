@@ -6,3 +6,5 @@ for v in nohist rephi; do
   python3 tools/sq_summary.py gpurun_out/r03w/$v/pass1/*counter_collection.csv gpurun_out/r03w/$v/pass2/*counter_collection.csv > gpurun_out/r03w/${v}_summary.txt
   rm -rf gpurun_out/r03w/$v/pass*/*.csv.gz
 done
+unset SIFT_HIP_LIB
+bash tools/bench_ab.sh r03w/ab 6 base SIFT_HIP_LIB=$L/extnt/libsift_hip.so SIFT_LDS_PX=2100
