@@ -424,6 +424,8 @@ def main() -> int:
                     help="time the pyramid/extrema launches of every k-th job of the timed "
                          "region with HIP events (per-launch events on every job slow the "
                          "pipeline by ~5%%)")
+    ap.add_argument("--step-log", action="store_true",
+                    help="print the timed region's submit / fetch / done times to stderr")
     ap.add_argument("--no-alone", action="store_true",
                     help="skip the kernel-alone roofline legs (PMC sessions count only the "
                          "timed region's launches)")
@@ -492,8 +494,11 @@ def main() -> int:
 
     sample_events = False  # set for the timed region
 
+    step_log = []  # --step-log: (event, job, t) of the timed region
+
     def run(n_steps: int) -> int:
         kp = 0
+        log = step_log.append if (args.step_log and sample_events) else None
         if args.sync:
             for k in range(n_steps):
                 if sample_events:
@@ -505,8 +510,14 @@ def main() -> int:
             while len(q) < depth and k + len(q) < n_steps:
                 if sample_events:
                     ctx.set_profiling((k + len(q)) % args.events_every == 0)
+                if log:
+                    log(("submit", k + len(q), time.perf_counter()))
                 q.append(submit())
+            if log:
+                log(("fetch", k, time.perf_counter()))
             kp += finish(q.popleft())
+            if log:
+                log(("done", k, time.perf_counter()))
         return kp
 
     run(max(1, args.warmup))
@@ -532,6 +543,10 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if step_log:
+        print("step log (ms from the timed region's start):", file=sys.stderr)
+        for ev, k, t in step_log:
+            print(f"  {ev:6s} job {k:3d} {1e3 * (t - t0):8.3f}", file=sys.stderr)
     sample_events = False
     ctx.set_profiling(False)
     prof = ctx.profile_table(reset=True)

@@ -280,18 +280,22 @@ struct sift_ctx {
     bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
     bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
     bool job_pairs = false;       // SIFT_JOB_STREAMS=2: two streams per job beyond the first
-    // SIFT_STREAM_POLICY (A/B knob; default 0): 0 = a job alone takes all
+    // SIFT_STREAM_POLICY (default 2). 0 = round 2: a job alone takes all
     // four pair streams, next to one other a free pair, else one free stream
-    // (pair streams first). 1 = pipelined jobs take one normal-priority
-    // stream each, and a caller seen pipelining keeps that when its pipeline
-    // is momentarily empty (pipe_hint); 2 = the same from the pair streams
-    // first. HIP gives each stream priority its own pool of at most
-    // GPU_MAX_HW_QUEUES hardware queues, shared by every stream of that
-    // priority in the process (torch's among them): policy 1 measured -4 %
-    // as the second context of an in-process A/B but +23 % as the bench's
-    // only context (0.72 vs 0.585 ms per step); policy 2 = policy 0 within
-    // noise (profiles/r03_e)
-    int stream_policy = 0;
+    // (pair streams first). 2 = a caller seen pipelining (pipe_hint: a job
+    // submitted next to another in the last kPipeHint submits) gets one
+    // stream per job, pair streams first, even when its pipeline is
+    // momentarily empty, so the next jobs of a burst do not share the first
+    // job's hardware queues. 1 = the same from the normal-priority pool
+    // first; 3 = from four high-priority streams. HIP pools hardware queues
+    // per stream priority (high: -1; normal: 0, shared with every default
+    // stream of the process, torch's included). Measured with the driver's
+    // bench command (20 steps, four in flight; profiles/r03_i): policy 2
+    // 0.586-0.593 ms per step, 0 0.582-0.640, 1 0.72 (normal pool shared
+    // with torch), 3 0.72-0.77 (four equal priorities: the four jobs in
+    // flight progress together and finish together, so the host waits a
+    // whole job latency every fourth step and refills in bursts)
+    int stream_policy = 2;
     int pipe_hint = 0;
     int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
@@ -1101,8 +1105,17 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
             !ctx->serial) {
             // one stream: policy 1 from the normal-priority pool first,
             // policy 2 from the four pair streams first; else any free one
-            int k = ctx->stream_policy == 1 ? 2 * kPairs : 0;
-            while (k < kSlots && (used >> k & 1u)) ++k;
+            int k = kSlots;
+            if (ctx->stream_policy == 3) {  // the four high-priority streams first
+                for (int c : {0, 1, 2 * kPairs, 2 * kPairs + 1})
+                    if (!(used >> c & 1u)) {
+                        k = c;
+                        break;
+                    }
+            } else {
+                k = ctx->stream_policy == 1 ? 2 * kPairs : 0;
+                while (k < kSlots && (used >> k & 1u)) ++k;
+            }
             if (k == kSlots) {
                 k = 0;
                 while (k + 1 < kSlots && (used >> k & 1u)) ++k;
@@ -1286,8 +1299,17 @@ int sift_hip_create(int device, sift_ctx** out) {
     ctx->pool[1] = ctx->pyr_stream[1];
     ctx->pool[2] = ctx->kp_stream[0];
     ctx->pool[3] = ctx->kp_stream[1];
-    for (int k = 2 * kPairs; k < kSlots; ++k)
-        ok = ok && hipStreamCreateWithFlags(&ctx->pool[k], hipStreamNonBlocking) == hipSuccess;
+    for (int k = 2 * kPairs; k < kSlots; ++k) {
+        // policy 3: two more high-priority streams, so pipelined jobs run on
+        // four streams of equal priority (HIP pools hardware queues per
+        // priority; the normal pool is shared with every other default-
+        // priority stream of the process, torch's included)
+        if (ctx->stream_policy == 3 && k < 2 * kPairs + 2)
+            ok = ok && hipStreamCreateWithPriority(&ctx->pool[k], hipStreamNonBlocking, prio_hi) ==
+                           hipSuccess;
+        else
+            ok = ok && hipStreamCreateWithFlags(&ctx->pool[k], hipStreamNonBlocking) == hipSuccess;
+    }
     for (Slot& s : ctx->slots) {
         ok = ok && hipMalloc(&s.d_ctr, kCtrWords * sizeof(unsigned)) == hipSuccess &&
              hipHostMalloc(&s.h_ctr, 4 * kLanes * sizeof(unsigned)) == hipSuccess &&
