@@ -38,6 +38,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <initializer_list>
 #include <new>
@@ -159,6 +160,19 @@ struct EventPair {
 
 enum SlotState { kFree = 0, kSubmitted = 1, kFinalized = 2 };
 
+// Everything a job's stream work depends on: its shape and parameters, its
+// inputs (device pointers; host bytes go through the slot's pinned staging)
+// and the slot's buffers (grow-only: same pointers and capacities). Not the
+// stream: a graph is launched on whichever stream the job was given.
+// Compared bytewise (zero-initialised, so padding is zero).
+struct GraphKey {
+    int n_img, kind, w, h, c, want_df;
+    sift_params p;
+    const void* img[SIFT_MAX_BATCH];
+    const void* buf[12];
+    size_t cap[6];
+};
+
 // Everything one job owns; reused (grow-only) by later jobs in this slot.
 struct Slot {
     int state = kFree;
@@ -207,6 +221,19 @@ struct Slot {
     int lanes = kLanes;
     int o_big = 0;  // octaves below: wavefront-per-keypoint kernels (enqueue_job)
     std::vector<EventPair> pending;
+    // launch graph of this slot's job (enqueue_job_graph): valid while the
+    // key (job shape, streams, inputs, buffer state) repeats
+    GraphKey gkey{};
+    bool gvalid = false;
+    // the job as graph segments, each followed by the event that ends it
+    // (chain ends, done): events are recorded between segment launches,
+    // since HIP rejects event records captured into a graph
+    std::vector<hipGraphExec_t> gseg;
+    std::vector<hipEvent_t> gseg_ev;
+    int g_nchains = 0;
+    std::vector<int> g_chain_lane;
+    bool capturing = false;
+    hipStream_t capture_stream = nullptr;
     // finalize
     bool exported = true;
     unsigned n_lane[kLanes] = {};
@@ -296,6 +323,12 @@ struct sift_ctx {
     // flight progress together and finish together, so the host waits a
     // whole job latency every fourth step and refills in bursts)
     int stream_policy = 2;
+    // SIFT_GRAPHS=1: pipelined jobs through per-slot launch graphs
+    // (enqueue_job_graph). Off by default: the host's enqueue drops from
+    // 0.12 to 0.03-0.04 ms per 1080p job, but the driver's bench command ran
+    // 0.596 / 0.610 ms per step against 0.584 / 0.590 eager (the host is not
+    // the bottleneck at four jobs in flight; profiles/r03_j)
+    bool graphs = false;
     int pipe_hint = 0;
     int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
@@ -333,10 +366,24 @@ struct sift_ctx {
 
 namespace {
 
-#define SIFT_HIP_TRY(expr)                          \
-    do {                                            \
-        hipError_t e_ = (expr);                     \
-        if (e_ != hipSuccess) return SIFT_ERR_HIP;  \
+// SIFT_DEBUG=1: report the failing HIP call on stderr
+bool debug_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("SIFT_DEBUG");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+#define SIFT_HIP_TRY(expr)                                                              \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            if (debug_enabled())                                                        \
+                std::fprintf(stderr, "sift_hip: %s:%d: %s: %s\n", __FILE__, __LINE__, #expr, \
+                             hipGetErrorString(e_));                                   \
+            return SIFT_ERR_HIP;                                                        \
+        }                                                                               \
     } while (0)
 
 hipEvent_t pool_event(Slot& s) {  // timing events (profiling)
@@ -432,6 +479,36 @@ void abandon(sift_ctx* ctx, Slot& s) {
     s.pending.clear();
     s.state = kFree;
     s.ticket = -1;
+}
+
+// Record `e` on stream `st`. While a job is being captured (enqueue_job_graph)
+// this ends the current graph segment, launches it, records the event
+// eagerly and begins the next segment.
+hipError_t record_event(Slot& s, hipEvent_t e, hipStream_t st) {
+    if (!s.capturing) return hipEventRecord(e, st);
+    hipGraph_t graph = nullptr;
+    hipError_t r = hipStreamEndCapture(s.capture_stream, &graph);
+    hipGraphExec_t exec = nullptr;
+    if (r == hipSuccess) r = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (graph) (void)hipGraphDestroy(graph);
+    if (r != hipSuccess) {
+        s.capturing = false;
+        return r;
+    }
+    s.gseg.push_back(exec);
+    s.gseg_ev.push_back(e);
+    if ((r = hipGraphLaunch(exec, s.capture_stream)) != hipSuccess ||
+        (r = hipEventRecord(e, s.capture_stream)) != hipSuccess ||
+        (r = hipStreamBeginCapture(s.capture_stream, hipStreamCaptureModeRelaxed)) != hipSuccess)
+        s.capturing = false;
+    return r;
+}
+
+void drop_graph(Slot& s) {
+    for (hipGraphExec_t x : s.gseg) (void)hipGraphExecDestroy(x);
+    s.gseg.clear();
+    s.gseg_ev.clear();
+    s.gvalid = false;
 }
 
 // One keypoint chain: extrema over octaves [o_begin, o_end) -> refine ->
@@ -753,7 +830,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                                      s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
                                      (unsigned)s.exp_lane}};
         if ((st = enqueue_chain(ctx, s, c)) != SIFT_OK) return st;
-        SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], c.sx));
+        SIFT_HIP_TRY(record_event(s, s.chain_ev[ci], c.sx));
         return SIFT_OK;
     };
     int n_batches = 0;
@@ -831,8 +908,132 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     }
     SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                 hipMemcpyDeviceToHost, sC));
-    SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
+    SIFT_HIP_TRY(record_event(s, s.done_ev, sC));
     s.t_host[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return SIFT_OK;
+}
+
+// Every buffer enqueue_job grows, sized up front with the same requests, so
+// that a job's enqueue allocates nothing (graph capture: enqueue_job_graph).
+int prepare_buffers(Slot& s, int kind) {
+    const Geometry& g = s.g;
+    const int n_img = s.n_img;
+    const size_t ne = (size_t)s.w * s.h * s.c;
+    int st;
+    if (!(kind == SIFT_INPUT_F64_DEVICE && n_img == 1)) {
+        if ((st = s.in.ensure(ne * n_img)) != SIFT_OK) return st;
+        if (kind == SIFT_INPUT_F64_HOST || kind == SIFT_INPUT_U8_HOST) {
+            if ((st = s.h_up.ensure(ne * n_img * sizeof(double))) != SIFT_OK) return st;
+            if ((st = s.in8.ensure(ne * n_img)) != SIFT_OK) return st;
+        }
+    }
+    if ((st = s.pyr.ensure(g.total * n_img)) != SIFT_OK) return st;
+    bool wide = s.taps_init.R > kMaxTemplR || s.taps_init.R < 1;
+    for (int l = 1; l < g.n_gauss; ++l) wide |= s.taps[l].R > kMaxTemplR || s.taps[l].R < 1;
+    if (wide && (st = s.tmp.ensure(2 * (size_t)g.W[0] * g.H[0] * n_img)) != SIFT_OK) return st;
+    const size_t want_cand =
+        std::min<size_t>(std::max<size_t>(g.sum_px * n_img / 32, 65536), kMaxCand);
+    if ((st = ensure_kp_arrays(s, std::max(s.cap_cand, want_cand), std::max(s.cap_raw, want_cand),
+                               std::max(s.cap_ori, 2 * want_cand))) != SIFT_OK)
+        return st;
+    const size_t exp_want = std::max<size_t>(s.exp_rec.cap, (size_t)8192 * n_img * kLanes);
+    if ((st = s.exp_rec.ensure(exp_want)) != SIFT_OK ||
+        (st = s.exp_side.ensure(s.exp_rec.cap)) != SIFT_OK ||
+        (st = s.exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
+        return st;
+    return SIFT_OK;
+}
+
+GraphKey graph_key(const Slot& s, const void* const* images, int kind) {
+    GraphKey k;
+    std::memset(&k, 0, sizeof k);
+    k.n_img = s.n_img;
+    k.kind = kind;
+    k.w = s.w;
+    k.h = s.h;
+    k.c = s.c;
+    k.want_df = s.want_df;
+    k.p = s.p;
+    const bool dev = kind == SIFT_INPUT_F64_DEVICE || kind == SIFT_INPUT_U8_DEVICE;
+    for (int b = 0; b < s.n_img && dev; ++b) k.img[b] = images[b];
+    const void* buf[12] = {s.in.p, s.in8.p, s.pyr.p, s.tmp.p, s.cand.p, s.raw.p,
+                           s.ori.p, s.side.p, s.df32.p, s.exp_rec.d, s.exp_side.d, s.h_up.p};
+    std::memcpy(k.buf, buf, sizeof buf);
+    const size_t cap[6] = {s.cap_cand, s.cap_raw, s.cap_ori, s.exp_rec.cap, s.exp_cnt.cap,
+                           s.h_up.cap};
+    std::memcpy(k.cap, cap, sizeof cap);
+    return k;
+}
+
+// A job's launches through a per-slot hipGraph: the host cost of ~38
+// launches and copies (0.11-0.15 ms per 1080p job) becomes one graph launch.
+// Single-stream jobs only (the pipelined case; a job alone on the chip runs
+// its pyramid octaves and keypoint lanes on four streams, eagerly), device
+// or byte inputs (a host Image of doubles may or may not pack to bytes),
+// never with profiling events or lab knobs. prepare_buffers sizes every
+// buffer first, so the capture allocates nothing; a job whose key matches
+// the slot's graph replays it, another captures its own. A replay repeats only the host side of
+// enqueue_job: the input bytes for host images and the export poison.
+int enqueue_job_graph(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
+    const bool single = s.sA == s.sB && s.sA == s.sC && s.sA == s.sD;
+    int st = prepare_buffers(s, kind);
+    if (st != SIFT_OK) return st;
+    const GraphKey key = graph_key(s, images, kind);
+    const bool match = s.gvalid && std::memcmp(&key, &s.gkey, sizeof key) == 0;
+    if (!ctx->graphs || !single || ctx->profiling || ctx->lab_double ||
+        kind == SIFT_INPUT_F64_HOST) {
+        // an eager job of another key rewrites the slot's host staging (the
+        // pyramid table the graph's first copy uploads): the graph is stale
+        if (!match) s.gvalid = false;
+        return enqueue_job(ctx, s, images, kind);
+    }
+    hipStream_t stream = s.sA;
+    if (match) {
+        const auto t0 = clk::now();
+        s.t_submit = t0;
+        s.ev_i = 0;
+        s.ev_used = 0;
+        s.pending.clear();
+        s.n_chains = s.g_nchains;
+        s.chain_lane = s.g_chain_lane;
+        if (kind == SIFT_INPUT_U8_HOST) {  // the staging the graph's first copy reads
+            const size_t ne = (size_t)s.w * s.h * s.c;
+            for (int b = 0; b < s.n_img; ++b) std::memcpy(s.h_up.p + b * ne, images[b], ne);
+        }
+        std::fill(s.exp_cnt.h, s.exp_cnt.h + s.exp_cnt.cap, 0xFFFFFFFFu);
+        for (size_t i = 0; i < s.gseg.size(); ++i) {
+            SIFT_HIP_TRY(hipGraphLaunch(s.gseg[i], stream));
+            SIFT_HIP_TRY(hipEventRecord(s.gseg_ev[i], stream));
+        }
+        s.t_host[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        return SIFT_OK;
+    }
+    // capture this job's launches segment by segment (record_event launches
+    // each segment as it closes), keep the segments for the next jobs
+    drop_graph(s);
+    SIFT_HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    s.capturing = true;
+    s.capture_stream = stream;
+    st = enqueue_job(ctx, s, images, kind);
+    const bool ok = s.capturing;  // false: a segment failed (capture ended)
+    s.capturing = false;
+    if (ok) {  // the empty capture after the last event
+        hipGraph_t graph = nullptr;
+        const hipError_t ce = hipStreamEndCapture(stream, &graph);
+        if (graph) (void)hipGraphDestroy(graph);
+        if (st == SIFT_OK && ce != hipSuccess) st = SIFT_ERR_HIP;
+    } else if (st == SIFT_OK) {
+        st = SIFT_ERR_HIP;
+    }
+    if (st != SIFT_OK) {
+        drop_graph(s);
+        if (debug_enabled()) std::fprintf(stderr, "sift_hip: graph capture failed (%d)\n", st);
+        return st;
+    }
+    s.gkey = key;
+    s.gvalid = true;
+    s.g_nchains = s.n_chains;
+    s.g_chain_lane = s.chain_lane;
     return SIFT_OK;
 }
 
@@ -1159,7 +1360,7 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
         }
     }
     s.state = kSubmitted;
-    st = enqueue_job(ctx, s, images, kind);
+    st = enqueue_job_graph(ctx, s, images, kind);
     if (st != SIFT_OK) {
         abandon(ctx, s);
         return st;
@@ -1280,6 +1481,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_ORI_MODE")) ctx->ori_mode = std::atoi(e);
     if (const char* e = std::getenv("SIFT_JOB_STREAMS")) ctx->job_pairs = std::atoi(e) == 2;
     if (const char* e = std::getenv("SIFT_STREAM_POLICY")) ctx->stream_policy = std::atoi(e);
+    if (const char* e = std::getenv("SIFT_GRAPHS")) ctx->graphs = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_FUSE_INITIAL")) ctx->fuse_initial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_EXTREMA_TILES")) ctx->extrema_stream = std::atoi(e) == 0;
@@ -1345,6 +1547,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
         s.side.release();
         s.df32.release();
         s.lab.release();
+        drop_graph(s);
         if (s.d_ctr) (void)hipFree(s.d_ctr);
         if (s.d_stage) (void)hipFree(s.d_stage);
         if (s.h_ctr) (void)hipHostFree(s.h_ctr);

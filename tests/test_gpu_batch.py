@@ -17,7 +17,8 @@ import pytest
 from golden_util import all_goldens
 from oracle_bind import OracleRun
 from parity import compare_final, final_ok
-from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, INPUT_U8_DEVICE, MAX_INFLIGHT, Context,
+from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, INPUT_U8_DEVICE, INPUT_U8_HOST, MAX_INFLIGHT,
+                      Context,
                       SiftParams,
                       synth_image)
 
@@ -288,3 +289,43 @@ def test_gpu_fetch_device_bulk_and_exported_paths():
                 assert int(chk.item()) == int(out[:n].view(-1).view(torch.int64).sum().item())
     finally:
         ctx.close()
+
+
+def test_gpu_graph_replay_equals_eager():
+    """Pipelined single-stream jobs go through a per-slot launch graph
+    (captured on a slot's first job of a shape, replayed after): many jobs
+    of two shapes, device and byte inputs, interleaved so slots switch
+    shapes, must give the same records as a context with graphs off."""
+    import torch
+
+    shapes = [(640, 480, 1), (333, 251, 3)]
+    imgs = [synth_image(w, h, c, seed=900 + i) for i, (w, h, c) in enumerate(shapes)]
+    dev = [torch.from_numpy(im).cuda() for im in imgs]
+    u8 = [np.ascontiguousarray(np.rint(im).clip(0, 255).astype(np.uint8)) for im in imgs]
+    torch.cuda.synchronize()
+    eager = Context(0)
+    os.environ["SIFT_GRAPHS"] = "1"
+    try:
+        graphed = Context(0)
+    finally:
+        del os.environ["SIFT_GRAPHS"]
+    try:
+        ref = {}
+        for i, (w, h, c) in enumerate(shapes):
+            ref[("dev", i)] = eager.detect_device(dev[i].data_ptr(), w, h, c)[0]
+            ref[("u8", i)] = eager.detect_u8(u8[i])[0]
+        order = [(kind, i % 2) for i in range(24) for kind in ("dev", "u8")]
+        q = []
+        for kind, i in order:
+            w, h, c = shapes[i]
+            if len(q) == 4:
+                key, t = q.pop(0)
+                _assert_same_records(graphed.fetch(t)[0][0], ref[key])
+            src = [dev[i].data_ptr()] if kind == "dev" else [u8[i]]
+            q.append(((kind, i), graphed.submit(src, INPUT_F64_DEVICE if kind == "dev"
+                                                else INPUT_U8_HOST, w, h, c)))
+        for key, t in q:
+            _assert_same_records(graphed.fetch(t)[0][0], ref[key])
+    finally:
+        graphed.close()
+        eager.close()
