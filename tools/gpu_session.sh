@@ -5,6 +5,10 @@
 # bench  the driver's exact bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 # prof   rocprofv3 --kernel-trace --stats of that same command, plus a
 #        serialised (SIFT_SERIAL=1, kernel-alone) trace; summaries via prof_summary.py
+# timeline  kernel trace of synchronous detects (the latency critical path)
+# steplog   the timed region's job timeline (bench.py --step-log)
+# ab/ab2/ab3  in-process interleaved A/B ($AB_ARGS ...); for anything that
+#        touches streams use tools/bench_ab.sh (one process per run)
 # Every GPU step has its own time limit and the steps stop at the first failure.
 set -o pipefail
 R=$(pwd)
@@ -45,6 +49,24 @@ for step in "$@"; do
     timeout -k 10 600 python -u tools/ab_interleaved.py ${!v} > $O/$step.txt 2>&1 \
         || { tail -20 $O/$step.txt; exit 1; }
     grep -v amdgpu.ids $O/$step.txt ;;
+  timeline)
+    # kernels of synchronous detects on their real streams (start / end /
+    # queue per dispatch of one image): the latency critical path
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/$O/lat -o run \
+        -- python3 $R/bench.py --sync --steps 100 --warmup 10 --no-cpu-baseline --no-extra \
+        --no-matcher --no-alone --no-desc-f64 --no-events > $R/$O/bench_lat.json 2> $R/$O/bench_lat.err \
+        || { tail -20 $R/$O/bench_lat.err; exit 1; }
+    cd $R
+    python tools/prof_summary.py $O/lat/run_kernel_trace.csv > $O/summary_lat.txt
+    rm -rf $O/lat
+    tail -45 $O/summary_lat.txt ;;
+  steplog)
+    # the driver's bench shape with the timed region's submit / fetch / done times
+    timeout -k 10 120 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-matcher \
+        --no-alone --no-desc-f64 --no-extra --step-log > $O/steplog.json 2> $O/steplog.err \
+        || { tail -20 $O/steplog.err; exit 1; }
+    grep -A70 "step log" $O/steplog.err ;;
   divcheck)
     timeout -k 10 300 tools/divcheck > $O/divcheck.txt 2>&1 || { tail -5 $O/divcheck.txt; exit 1; }
     tail -3 $O/divcheck.txt ;;
