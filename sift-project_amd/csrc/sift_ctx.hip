@@ -329,6 +329,11 @@ struct sift_ctx {
     // 0.596 / 0.610 ms per step against 0.584 / 0.590 eager (the host is not
     // the bottleneck at four jobs in flight; profiles/r03_j)
     bool graphs = false;
+    // SIFT_AGE_PRIO (A/B knob): kernels raise their waves' issue priority by
+    // their job's age rank (JobPrio); d_done counts the context's completed
+    // jobs (k_job_done at the end of every job)
+    bool age_prio = true;
+    unsigned* d_done = nullptr;
     int pipe_hint = 0;
     int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
@@ -677,6 +682,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     s.h_pt.img_stride = stride;
     s.h_pt.n_img = n_img;
     s.h_pt.n_oct = g.octaves;
+    s.h_pt.jp = s.taps_init.jp;
     // the slot's previous job has been fetched, so its copy out of h_stage
     // has completed and the staging can be rewritten
     s.h_stage->pt = s.h_pt;
@@ -909,6 +915,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         SIFT_HIP_TRY(hipEventRecord(jd, sD));
         SIFT_HIP_TRY(hipStreamWaitEvent(sC, jd, 0));
     }
+    if (s.taps_init.jp.done) SIFT_HIP_TRY(launch_job_done(ctx->d_done, sC));
     SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                 hipMemcpyDeviceToHost, sC));
     SIFT_HIP_TRY(record_event(s, s.done_ev, sC));
@@ -1279,6 +1286,9 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     }
     int st = host_plan(p, w, h, c, &s.g, &s.taps_init, s.taps, &s.dp);
     if (st != SIFT_OK) return st;
+    const JobPrio jp{(ctx->age_prio && !ctx->graphs) ? ctx->d_done : nullptr, ctx->next_ticket, 0};
+    s.taps_init.jp = jp;
+    for (BlurTaps& t : s.taps) t.jp = jp;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
     if (ctx->last == (int)(&s - ctx->slots)) ctx->last = -1;  // its buffers get reused
     s.n_img = n_images;
@@ -1485,6 +1495,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_JOB_STREAMS")) ctx->job_pairs = std::atoi(e) == 2;
     if (const char* e = std::getenv("SIFT_STREAM_POLICY")) ctx->stream_policy = std::atoi(e);
     if (const char* e = std::getenv("SIFT_GRAPHS")) ctx->graphs = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_AGE_PRIO")) ctx->age_prio = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_FUSE_INITIAL")) ctx->fuse_initial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_EXTREMA_TILES")) ctx->extrema_stream = std::atoi(e) == 0;
@@ -1493,6 +1504,8 @@ int sift_hip_create(int device, sift_ctx** out) {
         ctx->tile_max_px = t < 0 ? 0 : (size_t)1 << std::min(t, 40);
     }
     bool ok = prepare_kernel_attributes() == hipSuccess;
+    ok = ok && hipMalloc(&ctx->d_done, sizeof(unsigned)) == hipSuccess &&
+         hipMemset(ctx->d_done, 0, sizeof(unsigned)) == hipSuccess;
     for (int k = 0; k < kPairs; ++k)
         ok = ok &&
              hipStreamCreateWithPriority(&ctx->pyr_stream[k], hipStreamNonBlocking, prio_hi) ==
@@ -1579,6 +1592,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
     }
     for (int k = 2 * kPairs; k < kSlots; ++k)
         if (ctx->pool[k]) (void)hipStreamDestroy(ctx->pool[k]);
+    if (ctx->d_done) (void)hipFree(ctx->d_done);
     delete ctx;
     return SIFT_OK;
 }

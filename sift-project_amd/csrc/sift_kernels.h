@@ -57,6 +57,8 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_i
 // Keypoint stages process the index range [*begin, *end) of their input
 // list (device counters), so a detect can run them in batches.
 // snap[w] = ctr[w] for w in [w0, w1)
+// the context's completed-job counter += 1 (SIFT_AGE_PRIO)
+hipError_t launch_job_done(unsigned* done, hipStream_t s);
 hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, int w0 = 0,
                            int w1 = 4);
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,

@@ -51,6 +51,12 @@
 #ifndef SIFT_PRIO_LDS
 #define SIFT_PRIO_LDS 1
 #endif
+#ifndef SIFT_AGE_BOOST0  // SIFT_AGE_PRIO: issue-priority boost of the oldest job in flight
+#define SIFT_AGE_BOOST0 2
+#endif
+#ifndef SIFT_AGE_BOOST1  // ... and of the second oldest
+#define SIFT_AGE_BOOST1 1
+#endif
 #ifndef SIFT_EXT_PF
 #define SIFT_EXT_PF 2  // k_extrema_stream: rows in flight
 #endif
@@ -68,6 +74,25 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave issue priority of a kernel of job jp: `base` (the pyramid's static
+// priority), raised by 2 for the oldest job in flight and by 1 for the next
+// (rank from the context's completed-job counter, read once at start)
+__device__ __forceinline__ void set_job_prio(const JobPrio& jp, int base) {
+    int p = base;
+    if (jp.done) {
+        const int done = (int)__hip_atomic_load(jp.done, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        const int rank = jp.ticket - 1 - done;
+        p += rank <= 0 ? SIFT_AGE_BOOST0 : (rank == 1 ? SIFT_AGE_BOOST1 : 0);
+    }
+    switch (p < 3 ? p : 3) {
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        default: break;
+    }
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) {
@@ -208,7 +233,7 @@ template <int R, int C, bool DECIM, int MODE>
 __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict__ dst,
                                               size_t bs, int W, int H, int rows, BlurTaps taps,
                                               double* __restrict__ dec, int Wd, int Hd) {
-    if (SIFT_PRIO_STRIP > 0) __builtin_amdgcn_s_setprio(SIFT_PRIO_STRIP);
+    set_job_prio(taps.jp, SIFT_PRIO_STRIP);
     constexpr int PF = SIFT_BLUR_PF;               // rows in flight ahead of the staged one
     constexpr int NW = 2 * R + 2;                  // register window depth
     constexpr int SPAN = 64 * C;                   // strip width
@@ -424,7 +449,7 @@ __global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ sr
                                                    double* __restrict__ dst, size_t bs, int W,
                                                    int H, BlurTaps taps,
                                                    double* __restrict__ dec, int Wd, int Hd) {
-    if (SIFT_PRIO_TILE > 0) __builtin_amdgcn_s_setprio(SIFT_PRIO_TILE);
+    set_job_prio(taps.jp, SIFT_PRIO_TILE);
     constexpr int SH = kTileH + 2 * R;             // staged rows
     constexpr int SWp = (kTileW + 2 * R) | 1;      // staged row stride (odd)
     constexpr int RX = 4, RY = 8;                  // output runs per task
@@ -666,7 +691,7 @@ __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
 __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
                                                       int o_first, int o_last, int n_gauss,
                                                       const BlurTaps* __restrict__ taps) {
-    if (SIFT_PRIO_LDS > 0) __builtin_amdgcn_s_setprio(SIFT_PRIO_LDS);
+    set_job_prio(pt->jp, SIFT_PRIO_LDS);
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, nt = blockDim.x;
     const int dec_level = n_gauss - 3;
@@ -946,6 +971,7 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
                                                         sift_extremum* __restrict__ out,
                                                         unsigned* __restrict__ counter,
                                                         unsigned cap, unsigned* snap) {
+    set_job_prio(pt->jp, 0);
     constexpr int ND = NL - 1;   // DoG layers
     constexpr int NZ = ND - 2;   // layers with a full cube (z = 1 .. ND-2)
     constexpr int PF = SIFT_EXT_PF;  // rows in flight
@@ -1203,6 +1229,7 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
                                                 unsigned cap_cand, RawKp* __restrict__ out,
                                                 unsigned* __restrict__ n_out,
                                                 unsigned cap_out) {
+    set_job_prio(pt->jp, 0);
     __shared__ RefineLds T;
     const unsigned n = min(*n_cand, cap_cand);
     const unsigned i0 = min(*cand_begin, n);
@@ -1880,6 +1907,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
     sift_kp* __restrict__ recs, RecSide* __restrict__ rec_side, unsigned* __restrict__ n_rec,
     unsigned cap_rec, unsigned* __restrict__ work) {
     extern __shared__ double ori_wdyn[];
+    set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const unsigned n = min(*n_raw, cap_raw);
@@ -2134,6 +2162,7 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
     const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
     unsigned* __restrict__ work, ExportSink ex) {
     __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kDescWReps];
+    set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double* const hist = hist_all + wv * 128 * kDescWReps;
@@ -2685,6 +2714,13 @@ hipError_t launch_verify_slots(const void* slots, int n_slots, size_t slot_bytes
 __global__ void k_snapshot(const unsigned* __restrict__ ctr, unsigned* __restrict__ snap, int w0,
                            int w1) {
     if ((int)threadIdx.x >= w0 && (int)threadIdx.x < w1) snap[threadIdx.x] = ctr[threadIdx.x];
+}
+
+__global__ void k_job_done(unsigned* done) { atomicAdd(done, 1u); }
+
+hipError_t launch_job_done(unsigned* done, hipStream_t s) {
+    hipLaunchKernelGGL(k_job_done, dim3(1), dim3(1), 0, s, done);
+    return hipGetLastError();
 }
 
 hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, int w0, int w1) {

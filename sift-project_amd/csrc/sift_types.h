@@ -42,12 +42,22 @@ inline constexpr bool lds_octave_fits(int W, int H) {
 
 // Half kernel of apply_gaussian_blur_fast (image.cpp:226-235) plus its
 // normalising sum (image.cpp:171-185), computed on the host with glibc.
+// Age priority of a job's kernels (SIFT_AGE_PRIO): the kernel raises its
+// waves' issue priority by how close its job is to the oldest in flight,
+// rank = ticket - 1 - *done (done: jobs of the context completed so far)
+struct JobPrio {
+    const unsigned* done;  // nullptr: off
+    int ticket;
+    int pad;
+};
+
 struct BlurTaps {
     double k[kMaxTaps];
     double sum_w;
     double inv;  // RN(1 / sum_w), for the correctly rounded division
     int R;  // taps k[0..R], R = ks-1
     int pad;
+    JobPrio jp;
 };
 
 // What k_blur stages rows from: a W x H plane (p, with w = W), or the input
@@ -68,6 +78,7 @@ struct PyrTable {
     size_t img_stride;
     int n_img;
     int n_oct;
+    JobPrio jp;
 };
 
 // Streaming extrema tasks: centre columns per wavefront strip (64 lanes
