@@ -662,6 +662,12 @@ def main() -> int:
         if world == 1 and not args.no_desc_f64:
             leg = desc_modes_leg(ptrs, W, H, params, max(args.steps, 800), depth)
             out["value_desc_f64"] = leg["desc_mode_0"]["value"]
+            out["value_desc_f64_note"] = (
+                "steady state (desc_modes_leg: fresh contexts, interleaved blocks of pipelined "
+                "steps), not the 20-step shape of `value`; compare it with "
+                "desc_modes_leg.desc_mode_1, measured the same way: the all-f64 descriptor "
+                f"runs at {leg['desc_mode_0']['value'] / leg['desc_mode_1']['value']:.3f} of the "
+                "default's rate")
             leg["note"] = ("pipelined steps as the timed region, on two fresh contexts in "
                            "interleaved blocks: desc_mode 1 (default, f32 sample math) and "
                            "desc_mode 0 (all-f64 descriptor, the reference's precision)")

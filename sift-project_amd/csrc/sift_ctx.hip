@@ -578,9 +578,6 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     unsigned ori_wgs = std::min(ctx->kp_wgs_max, ctx->kp_wgs * (unsigned)n_img);
     unsigned desc_wgs = std::min(ctx->kp_wgs_max, ctx->desc_wgs * (unsigned)n_img);
     if (small) ori_wgs = desc_wgs = ctx->kp_wgs_small;
-    // SIFT_SERIAL (profiling: every kernel alone on the chip): grids that
-    // fill the chip, the kernel-alone view of the keypoint kernels
-    if (ctx->serial) ori_wgs = desc_wgs = std::max(ori_wgs, 1024u);
     if (lab) {
         SIFT_HIP_TRY(hipMemsetAsync(lab, 0, 8 * sizeof(unsigned), sx));
         if (ctx->lab_double & 2u)
