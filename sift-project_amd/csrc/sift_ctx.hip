@@ -334,6 +334,7 @@ struct sift_ctx {
     // jobs (k_job_done at the end of every job)
     bool age_prio = true;
     unsigned* d_done = nullptr;
+    DevBuf<unsigned long long> verify_acc;  // sift_hip_verify_slots: per-slot sums
     int pipe_hint = 0;
     int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
@@ -1589,6 +1590,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
     }
     for (int k = 2 * kPairs; k < kSlots; ++k)
         if (ctx->pool[k]) (void)hipStreamDestroy(ctx->pool[k]);
+    ctx->verify_acc.release();
     if (ctx->d_done) (void)hipFree(ctx->d_done);
     delete ctx;
     return SIFT_OK;
@@ -1670,9 +1672,11 @@ int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_
         return SIFT_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    if (ctx->verify_acc.ensure((size_t)std::max(n_slots, 1)) != SIFT_OK) return SIFT_ERR_NOMEM;
     SIFT_HIP_TRY(launch_verify_slots(d_slots, n_slots, slot_bytes, hdr_rows, count_word, sum_word,
                                      n_sum_words, cap_rows,
-                                     reinterpret_cast<unsigned long long*>(d_bad), st));
+                                     reinterpret_cast<unsigned long long*>(d_bad),
+                                     ctx->verify_acc.p, st));
     return SIFT_OK;
 }
 
