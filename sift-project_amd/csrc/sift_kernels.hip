@@ -1221,24 +1221,31 @@ __device__ bool refine_one(const RefineLds& T, size_t img_stride, const DevParam
 }
 
 // k_refine: candidates [cand_begin, n_cand), one thread each (the dependent
-// gathers of all candidates in flight together).
-__global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt, DevParams P,
-                                                const sift_extremum* __restrict__ cand,
-                                                const unsigned* __restrict__ cand_begin,
-                                                const unsigned* __restrict__ n_cand,
-                                                unsigned cap_cand, RawKp* __restrict__ out,
-                                                unsigned* __restrict__ n_out,
-                                                unsigned cap_out) {
+// gathers of all candidates in flight together). NT = 64 (default): one
+// wavefront per workgroup, so a batch's few thousand candidates spread over
+// ~100 CUs instead of ~25, and each CU's address units serve one wave's 36
+// scattered loads per step instead of four waves'.
+template <int NT, int CPW>
+__global__ __launch_bounds__(NT) void k_refine(const PyrTable* __restrict__ pt, DevParams P,
+                                               const sift_extremum* __restrict__ cand,
+                                               const unsigned* __restrict__ cand_begin,
+                                               const unsigned* __restrict__ n_cand,
+                                               unsigned cap_cand, RawKp* __restrict__ out,
+                                               unsigned* __restrict__ n_out,
+                                               unsigned cap_out) {
     set_job_prio(pt->jp, 0);
     __shared__ RefineLds T;
     const unsigned n = min(*n_cand, cap_cand);
     const unsigned i0 = min(*cand_begin, n);
-    const unsigned stride = gridDim.x * blockDim.x;
-    if (i0 + blockIdx.x * blockDim.x >= n) return;  // no candidate for this workgroup
+    // CPW candidates per wavefront (lanes >= CPW idle): fewer per wave
+    // spreads a batch over more CUs
+    constexpr int WPB = NT / 64;
+    const unsigned stride = gridDim.x * WPB * CPW;
+    if (i0 + blockIdx.x * WPB * CPW >= n) return;  // no candidate for this workgroup
     // grid-stride over whole waves (wave-uniform trip count), so the kept
     // keypoints of a wave take one counter atomic (ballot + prefix)
     const int lane = threadIdx.x & 63;
-    for (int k = threadIdx.x; k < kMaxOctaves * kMaxLevels; k += 256)
+    for (int k = threadIdx.x; k < kMaxOctaves * kMaxLevels; k += NT)
         T.lvl[k / kMaxLevels][k % kMaxLevels] = pt->lvl[k / kMaxLevels][k % kMaxLevels];
     if (threadIdx.x < kMaxOctaves) {
         T.w[threadIdx.x] = pt->w[threadIdx.x];
@@ -1246,12 +1253,12 @@ __global__ __launch_bounds__(256) void k_refine(const PyrTable* __restrict__ pt,
     }
     const size_t img_stride = pt->img_stride;
     __syncthreads();
-    for (unsigned i0w = i0 + blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0w < n;
+    for (unsigned i0w = i0 + (blockIdx.x * WPB + threadIdx.x / 64) * CPW; i0w < n;
          i0w += stride) {
         const unsigned i = i0w + lane;
         RawKp r;
         bool keep = false;
-        if (i < n) {
+        if (lane < CPW && i < n) {
             const sift_extremum e = cand[i];
             const int o = e.octave & ((1 << kOctBits) - 1), im = e.octave >> kOctBits;
             keep = refine_one(T, img_stride, P, e.x, e.y, e.z, o, im, &r);
@@ -2830,15 +2837,36 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_i
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s) {
-    static const unsigned max_blocks = [] {  // SIFT_REFINE_WGS: A/B knob
-        const char* e = std::getenv("SIFT_REFINE_WGS");
-        return e ? (unsigned)std::max(1, std::atoi(e)) : 1024u;
+    // SIFT_REFINE_NT (64 or 256 threads per workgroup), SIFT_REFINE_WGS: A/B knobs
+    static const int nt = [] {
+        const char* e = std::getenv("SIFT_REFINE_NT");
+        return (e && std::atoi(e) == 256) ? 256 : 64;
     }();
-    unsigned blocks = (cap_cand + 255) / 256;
+    static const int cpw = [] {  // SIFT_REFINE_CPW: candidates per wavefront (64, 32, 16)
+        const char* e = std::getenv("SIFT_REFINE_CPW");
+        const int v = e ? std::atoi(e) : 64;
+        return v == 16 ? 16 : v == 32 ? 32 : 64;
+    }();
+    static const unsigned max_blocks = [] {
+        const char* e = std::getenv("SIFT_REFINE_WGS");
+        return e ? (unsigned)std::max(1, std::atoi(e)) : 262144u / nt;
+    }();
+    const unsigned per_wg = (unsigned)(nt / 64 * cpw);
+    unsigned blocks = (cap_cand + per_wg - 1) / per_wg;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(k_refine, dim3(blocks), dim3(256), 0, s, d_pt, P, cand, cand_begin, n_cand,
-                       cap_cand, out, n_out, cap_out);
+#define SIFT_REFINE_LAUNCH(NT_, CPW_)                                                          \
+    hipLaunchKernelGGL((k_refine<NT_, CPW_>), dim3(blocks), dim3(NT_), 0, s, d_pt, P, cand,   \
+                       cand_begin, n_cand, cap_cand, out, n_out, cap_out)
+    if (nt == 256)
+        SIFT_REFINE_LAUNCH(256, 64);
+    else if (cpw == 16)
+        SIFT_REFINE_LAUNCH(64, 16);
+    else if (cpw == 32)
+        SIFT_REFINE_LAUNCH(64, 32);
+    else
+        SIFT_REFINE_LAUNCH(64, 64);
+#undef SIFT_REFINE_LAUNCH
     return hipGetLastError();
 }
 
