@@ -277,6 +277,9 @@ struct sift_ctx {
     unsigned desc_wgs = 192;
     unsigned kp_wgs_max = 512;
     unsigned kp_wgs_small = 512;   // SIFT_KP_WGS_SMALL: workgroup-per-keypoint chains
+    // a job alone on the chip (two keypoint lanes): per image, 0 = kp_wgs /
+    // desc_wgs (SIFT_KP_WGS_ALONE)
+    unsigned kp_wgs_alone = 0;
     // octaves of fewer pixels per image use the workgroup-per-keypoint
     // orientation / descriptor kernels (SIFT_KP_SMALL_PX; 0: never). Off:
     // at 2^20 (1080p octaves >= 2) the extra chain cost 3.6 % pipelined
@@ -576,8 +579,11 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     const bool small = o_begin >= s.o_big;
     const int ori_mode = (small && ctx->ori_mode == 1) ? 0 : ctx->ori_mode;
     const int desc_mode = (small && ctx->desc_mode == 1) ? 3 : ctx->desc_mode;
-    unsigned ori_wgs = std::min(ctx->kp_wgs_max, ctx->kp_wgs * (unsigned)n_img);
-    unsigned desc_wgs = std::min(ctx->kp_wgs_max, ctx->desc_wgs * (unsigned)n_img);
+    const bool alone = s.lanes > 1 && ctx->kp_wgs_alone;
+    unsigned ori_wgs = std::min(ctx->kp_wgs_max,
+                                (alone ? ctx->kp_wgs_alone : ctx->kp_wgs) * (unsigned)n_img);
+    unsigned desc_wgs = std::min(ctx->kp_wgs_max,
+                                 (alone ? ctx->kp_wgs_alone : ctx->desc_wgs) * (unsigned)n_img);
     if (small) ori_wgs = desc_wgs = ctx->kp_wgs_small;
     if (lab) {
         SIFT_HIP_TRY(hipMemsetAsync(lab, 0, 8 * sizeof(unsigned), sx));
@@ -1477,6 +1483,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_KP_WGS_MAX")) ctx->kp_wgs_max = (unsigned)std::atoi(e);
     if (ctx->kp_wgs_max < 1) ctx->kp_wgs_max = 1;
     if (const char* e = std::getenv("SIFT_KP_WGS_SMALL")) ctx->kp_wgs_small = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_KP_WGS_ALONE")) ctx->kp_wgs_alone = (unsigned)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_KP_SMALL_PX")) ctx->kp_small_px = (size_t)std::atoll(e);
     if (const char* e = std::getenv("SIFT_DESC_WGS")) ctx->desc_wgs = (unsigned)std::atoi(e);
     if (const char* e = std::getenv("SIFT_LAB_DOUBLE")) ctx->lab_double = (unsigned)std::atoi(e);
