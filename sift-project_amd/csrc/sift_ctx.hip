@@ -1284,10 +1284,10 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     if (!sp && ctx->last >= 0 && ctx->slots[ctx->last].state == kFree) sp = &ctx->slots[ctx->last];
     if (!sp) return SIFT_ERR_STATE;  // SIFT_MAX_INFLIGHT jobs already in flight
     Slot& s = *sp;
-    if (s.gather_pending) {  // an async device fetch may still read its records
-        SIFT_HIP_TRY(hipEventSynchronize(s.gather_ev));
-        s.gather_pending = false;
-    }
+    // an async device fetch may still read this slot's records: the new
+    // job's streams wait for it on the device (below), not the host
+    const bool gather_wait = s.gather_pending;
+    s.gather_pending = false;
     int st = host_plan(p, w, h, c, &s.g, &s.taps_init, s.taps, &s.dp);
     if (st != SIFT_OK) return st;
     const JobPrio jp{(ctx->age_prio && !ctx->graphs) ? ctx->d_done : nullptr, ctx->next_ticket, 0};
@@ -1376,6 +1376,14 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
             s.lanes = 1;
         }
     }
+    if (gather_wait) {
+        const hipStream_t js[4] = {s.sA, s.sB, s.sC, s.sD};
+        for (int i = 0; i < 4; ++i) {
+            bool dup = false;
+            for (int j = 0; j < i; ++j) dup |= js[j] == js[i];
+            if (!dup) SIFT_HIP_TRY(hipStreamWaitEvent(js[i], s.gather_ev, 0));
+        }
+    }
     s.state = kSubmitted;
     st = enqueue_job_graph(ctx, s, images, kind);
     if (st != SIFT_OK) {
@@ -1410,8 +1418,8 @@ void gather(Slot& s, sift_kp* out, float* df) {
 // final records of a finalised job into device memory, enqueued on the
 // slot's keypoint stream; `consumer` (optional) is ordered after the gather
 // by an event, so the caller's stream can use d_out with no host wait. The
-// slot's buffers stay in use until gather_ev, which a reuse of the slot waits
-// for (submit_impl).
+// slot's buffers stay in use until gather_ev, which the streams of the slot's next
+// job wait for on the device (submit_impl).
 int gather_device(Slot& s, sift_kp* d_out, hipStream_t consumer, unsigned long long* checksum) {
     const size_t n = s.n_final;
     int st;
