@@ -340,7 +340,10 @@ struct sift_ctx {
     DevBuf<unsigned long long> verify_acc;  // sift_hip_verify_slots: per-slot sums
     int pipe_hint = 0;
     int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
-    int desc_mode = 1;            // SIFT_DESC_MODE: 0 f64, 1 wave per record (f32 math), 2 f32 hist, 3 f32 math
+    // SIFT_DESC_MODE: 0 = k_descriptor_split, f64 sample math (default, the
+    // reference's arithmetic); A/B only: 1 = k_descriptor_wave (f32 sample
+    // math, a wavefront per record), 2 = k_descriptor_split with f32 math
+    int desc_mode = 0;
     int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
     // two stream pairs, one per hardware queue each (HIP's default is four
@@ -578,7 +581,7 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     // concurrent small-octave blurs on the critical path, 1.03 vs 0.95 ms)
     const bool small = o_begin >= s.o_big;
     const int ori_mode = (small && ctx->ori_mode == 1) ? 0 : ctx->ori_mode;
-    const int desc_mode = (small && ctx->desc_mode == 1) ? 3 : ctx->desc_mode;
+    const int desc_mode = ctx->desc_mode;
     const bool alone = s.lanes > 1 && ctx->kp_wgs_alone;
     unsigned ori_wgs = std::min(ctx->kp_wgs_max,
                                 (alone ? ctx->kp_wgs_alone : ctx->kp_wgs) * (unsigned)n_img);

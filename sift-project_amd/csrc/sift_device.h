@@ -1,0 +1,86 @@
+// sift_device.h — device helpers shared by the kernel translation units
+// (sift_kernels.hip: pyramid, extrema, refine, orientation; sift_desc.hip:
+// descriptors). Internal to the library.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "sift_types.h"
+
+#ifndef SIFT_AGE_BOOST0  // SIFT_AGE_PRIO: issue-priority boost of the oldest job in flight
+#define SIFT_AGE_BOOST0 2
+#endif
+#ifndef SIFT_AGE_BOOST1  // ... and of the second oldest
+#define SIFT_AGE_BOOST1 1
+#endif
+
+namespace sift_amd {
+
+namespace {
+
+constexpr double kTwoPi = 6.283185307179586;  // M_PI2 (sift.hh:5)
+constexpr double kPi = 3.14159265358979323846;  // M_PI
+
+// Compiler-level ordering for LDS traffic exchanged between the lanes of ONE
+// wavefront (a wave's LDS instructions execute in order in hardware).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave issue priority of a kernel of job jp: `base` (the pyramid's static
+// priority), raised by 2 for the oldest job in flight and by 1 for the next
+// (rank from the context's completed-job counter, read once at start)
+__device__ __forceinline__ void set_job_prio(const JobPrio& jp, int base) {
+    int p = base;
+    if (jp.done) {
+        const int done = (int)__hip_atomic_load(jp.done, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        const int rank = jp.ticket - 1 - done;
+        p += rank <= 0 ? SIFT_AGE_BOOST0 : (rank == 1 ? SIFT_AGE_BOOST1 : 0);
+    }
+    switch (p < 3 ? p : 3) {
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        default: break;
+    }
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) {
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// 2^e for small integer e, exact (the reference uses std::pow(2, int)).
+__device__ __forceinline__ double pow2i(int e) { return ldexp(1.0, e); }
+
+// Pyramid planes are device (global) memory; pointers read from the PyrTable
+// are generic to the compiler, which would emit flat loads (counted in both
+// vmcnt and lgkmcnt). Viewing them in address space 1 gives global loads.
+typedef __attribute__((address_space(1))) const double gdouble;
+__device__ __forceinline__ gdouble* gbl(const double* p) { return (gdouble*)p; }
+
+// Plane of level l of octave o of image b of the job (one pyramid arena per
+// image, identical layouts img_stride doubles apart).
+__device__ __forceinline__ const double* plane(const PyrTable* pt, int b, int o, int l) {
+    return pt->lvl[o][l] + (size_t)b * pt->img_stride;
+}
+
+// Correctly rounded a / s for the per-kernel constant s = sum_w, with
+// inv = RN(1/s) from the host: q = RN(a*inv) is faithful and Markstein's
+// correction q + (a - q*s)*inv (residual exact by FMA) rounds to RN(a/s) —
+// the same final step as gfx950's own v_div_fmas sequence, without the
+// v_rcp_f64 / Newton / scaling part. Checked against IEEE division on
+// 2.5e12 random operands over every divisor the default pyramids use
+// (tools/blur_lab.hip divcheck, 0 mismatches); the pyramid parity tests
+// compare every level bit for bit.
+__device__ __forceinline__ double div_sum_w(double a, double s, double inv) {
+    const double q = a * inv;
+    const double r = __builtin_fma(-q, s, a);
+    return __builtin_fma(r, inv, q);
+}
+
+}  // namespace
+
+}  // namespace sift_amd

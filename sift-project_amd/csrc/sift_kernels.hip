@@ -21,20 +21,12 @@
 #include <type_traits>
 
 #include "sift_pow2.h"
+#include "sift_device.h"
 #include "sift_kernels.h"
 
 // compile-time A/B knobs (alternative builds, SIFT_HIP_LIB)
 #ifndef SIFT_BLUR_PF
 #define SIFT_BLUR_PF 2  // k_blur: source rows in flight ahead of the staged one
-#endif
-#ifndef SIFT_DESC_AHEAD
-#define SIFT_DESC_AHEAD 1  // k_descriptor: samples (x64) whose loads are in flight
-#endif
-#ifndef SIFT_DESC_OCC
-#define SIFT_DESC_OCC 5  // k_descriptor (f32 math): min workgroups per CU
-#endif
-#ifndef SIFT_DESC_REPS
-#define SIFT_DESC_REPS 4  // k_descriptor: f64 histogram replicas per wave
 #endif
 // wave issue priority (s_setprio) of the pyramid kernels, which share CUs
 // with the keypoint kernels' gather-bound waves (of their own job and of the
@@ -51,12 +43,6 @@
 #ifndef SIFT_PRIO_LDS
 #define SIFT_PRIO_LDS 1
 #endif
-#ifndef SIFT_AGE_BOOST0  // SIFT_AGE_PRIO: issue-priority boost of the oldest job in flight
-#define SIFT_AGE_BOOST0 2
-#endif
-#ifndef SIFT_AGE_BOOST1  // ... and of the second oldest
-#define SIFT_AGE_BOOST1 1
-#endif
 #ifndef SIFT_EXT_PF
 #define SIFT_EXT_PF 2  // k_extrema_stream: rows in flight
 #endif
@@ -64,55 +50,6 @@
 namespace sift_amd {
 
 namespace {
-
-constexpr double kTwoPi = 6.283185307179586;  // M_PI2 (sift.hh:5)
-constexpr double kPi = 3.14159265358979323846;  // M_PI
-
-// Compiler-level ordering for LDS traffic exchanged between the lanes of ONE
-// wavefront (a wave's LDS instructions execute in order in hardware).
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Wave issue priority of a kernel of job jp: `base` (the pyramid's static
-// priority), raised by 2 for the oldest job in flight and by 1 for the next
-// (rank from the context's completed-job counter, read once at start)
-__device__ __forceinline__ void set_job_prio(const JobPrio& jp, int base) {
-    int p = base;
-    if (jp.done) {
-        const int done = (int)__hip_atomic_load(jp.done, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-        const int rank = jp.ticket - 1 - done;
-        p += rank <= 0 ? SIFT_AGE_BOOST0 : (rank == 1 ? SIFT_AGE_BOOST1 : 0);
-    }
-    switch (p < 3 ? p : 3) {
-        case 1: __builtin_amdgcn_s_setprio(1); break;
-        case 2: __builtin_amdgcn_s_setprio(2); break;
-        case 3: __builtin_amdgcn_s_setprio(3); break;
-        default: break;
-    }
-}
-
-__device__ __forceinline__ int clampi(int v, int lo, int hi) {
-    return v < lo ? lo : (v > hi ? hi : v);
-}
-
-// 2^e for small integer e, exact (the reference uses std::pow(2, int)).
-__device__ __forceinline__ double pow2i(int e) { return ldexp(1.0, e); }
-
-// Pyramid planes are device (global) memory; pointers read from the PyrTable
-// are generic to the compiler, which would emit flat loads (counted in both
-// vmcnt and lgkmcnt). Viewing them in address space 1 gives global loads.
-typedef __attribute__((address_space(1))) const double gdouble;
-__device__ __forceinline__ gdouble* gbl(const double* p) { return (gdouble*)p; }
-
-// Plane of level l of octave o of image b of the job (one pyramid arena per
-// image, identical layouts img_stride doubles apart).
-__device__ __forceinline__ const double* plane(const PyrTable* pt, int b, int o, int l) {
-    return pt->lvl[o][l] + (size_t)b * pt->img_stride;
-}
 
 // XCD-aware block remap (bijective): workgroups are dealt round-robin over
 // the 8 XCDs, so consecutive block ids land on different L2s. Renumber so
@@ -189,20 +126,6 @@ __global__ __launch_bounds__(256) void k_prepare(const double* __restrict__ in, 
     const double v0 = gray(x0, y0) * (1 - dx) + gray(x1, y0) * dx;
     const double v1 = gray(x0, y1) * (1 - dx) + gray(x1, y1) * dx;
     out[(size_t)oy * W0 + ox] = v0 * (1 - dy) + v1 * dy;
-}
-
-// Correctly rounded a / s for the per-kernel constant s = sum_w, with
-// inv = RN(1/s) from the host: q = RN(a*inv) is faithful and Markstein's
-// correction q + (a - q*s)*inv (residual exact by FMA) rounds to RN(a/s) —
-// the same final step as gfx950's own v_div_fmas sequence, without the
-// v_rcp_f64 / Newton / scaling part. Checked against IEEE division on
-// 2.5e12 random operands over every divisor the default pyramids use
-// (tools/blur_lab.hip divcheck, 0 mismatches); the pyramid parity tests
-// compare every level bit for bit.
-__device__ __forceinline__ double div_sum_w(double a, double s, double inv) {
-    const double q = a * inv;
-    const double r = __builtin_fma(-q, s, a);
-    return __builtin_fma(r, inv, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -1323,35 +1246,7 @@ __global__ __launch_bounds__(NT) void k_refine(const PyrTable* __restrict__ pt, 
 //    reductions (the bins themselves are already summed out of the
 //    reference's order, so a sequential sum would buy no exactness).
 // ---------------------------------------------------------------------------
-// atan2 in f32 for the descriptor's sample math: octant reduction to
-// a = min(|x|, |y|) / max(|x|, |y|) (v_rcp_f32, 1 ulp), atan(a) as
-// a + a^3 p(a^2) with a degree-7 p fitted for minimum max error on [0, 1]
-// (8.5e-8 rad in f32 arithmetic over 2e6 points), then the quadrant fix-up.
-// About 20 VALU instructions against ~35 for atan2f; total error below
-// 2e-7 rad, i.e. < 3e-7 of a descriptor orientation bin (contract: 1e-4 on
-// the normalised floats). atan2(0, 0) = 0; signs of zeros as atan2f.
-__device__ __forceinline__ float atan2_f32(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
-    const float t = a * a;
-    float p = 0.0026222362648695707f;
-    p = fmaf(p, t, -0.015132501721382141f);
-    p = fmaf(p, t, 0.04112179949879646f);
-    p = fmaf(p, t, -0.0736670047044754f);
-    p = fmaf(p, t, 0.1057392954826355f);
-    p = fmaf(p, t, -0.1418597400188446f);
-    p = fmaf(p, t, 0.1999039649963379f);
-    p = fmaf(p, t, -0.33332985639572144f);
-    float th = fmaf(a * t, p, a);
-    if (ay > ax) th = 1.57079637f - th;
-    if (x < 0.0f) th = 3.14159274f - th;
-    return copysignf(th, y);
-}
-
 constexpr int kOriReps = 4;
-constexpr int kDescReps = SIFT_DESC_REPS;  // f64 histogram replicas per wave (power of 2)
-constexpr int kDescRepStride = 130;  // doubles; the pad rotates LDS banks
 // k_orient: the replicas (4 * kOriReps * (num_bins + 2) doubles) and the
 // Gaussian weight table (kOriTab doubles) live in dynamic LDS sized per
 // launch (17 KB at 36 bins), so orientation workgroups leave room on a CU for
@@ -1363,305 +1258,6 @@ struct KpLds {
     double red[4];         // normalisation partial sums
     unsigned k, npk, rec;
 };
-
-// LDS of k_descriptor. MODE 2: 16 lane-interleaved f32 replicas of the
-// 4x4x8 histogram per wave (33 KB); f64: 4 per wave (17 KB).
-constexpr int kDescRepsF = 16;
-struct DescLds {
-    float hist[4 * kDescRepsF * kDescRepStride];
-    double red[4];
-    unsigned k;
-};
-struct DescLds64 {
-    double hist[4 * kDescReps * kDescRepStride];
-    double red[4];
-    unsigned k;
-};
-// MODE: 0 = f64 sample math and histograms (4 replicas per wave);
-// 1 = f32 sample math, f64 histograms; 2 = f32 math and histograms (16 per wave)
-template <int MODE>
-using DescLdsT = typename std::conditional<MODE == 2, DescLds, DescLds64>::type;
-
-// One descriptor (sift.cpp:610-682) of record `rec`; all 256 threads.
-template <int MODE>
-__device__ void describe(DescLdsT<MODE>& S, const PyrTable* __restrict__ pt, const DevParams& P,
-                         sift_kp* __restrict__ recs, unsigned rec, double kx, double ky, int o,
-                         int layer, double ksize, double pori, RecSide rside,
-                         float* __restrict__ desc_f32, const ExportSink& ex) {
-    constexpr bool F32 = MODE != 0;
-    using HT = typename std::conditional<MODE == 2, float, double>::type;
-    constexpr int kReps = MODE == 2 ? kDescRepsF : kDescReps;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    HT* hw_rep = &S.hist[(wv * kReps + (lane & (kReps - 1))) * kDescRepStride];
-    gdouble* img = gbl(plane(pt, rside.img, o, layer));
-    const int W = pt->w[o], H = pt->h[o];
-    const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
-    const int x = (int)(kx * inv);
-    const int y = (int)(ky * inv);
-    const double size = ksize * inv;
-    const double bins_per_rad = kDescBins / kTwoPi;
-    const double ca = cos(pori), sa = sin(pori);
-    const double hw = P.desc_scale_factor * size;
-    const double ihw = 1.0 / hw;
-    const double denom = 0.5 * kDescW * kDescW;
-    const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
-    const double diag = sqrt((double)(W * W + H * H));
-    const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
-    const int side = 2 * radius + 1;
-    for (int i = tid; i < 4 * kReps * kDescRepStride; i += 256) S.hist[i] = (HT)0;
-    __syncthreads();
-    // f32 sample math: acceptance is decided exactly (f64) before a sample
-    // is processed; everything after it (bin position, gradient magnitude and
-    // angle, Gaussian weight, trilinear split) is continuous in its inputs,
-    // so f32 rounding moves a descriptor float by ~1e-7 (contract: 1e-4)
-    const float saf = (float)sa, caf = (float)ca, ihwf = (float)ihw;
-    const float porif = (float)pori;
-    const float wscale = (float)(-1.4426950408889634 / denom);  // -log2(e)/denom
-
-    // the reference's rotated-box + image-border test (sift.cpp:645-656)
-    auto accepted = [&](int row, int col) -> bool {
-        const double row_rot = div_sum_w(col * sa + row * ca, hw, ihw);
-        const double col_rot = div_sum_w(col * ca - row * sa, hw, ihw);
-        const double rb = row_rot + kDescW / 2 - 0.5;
-        const double cb = col_rot + kDescW / 2 - 0.5;
-        const int nx = col + x, ny = row + y;
-        return col >= -radius && col <= radius && rb > -1.0 && rb < kDescW && cb > -1.0 &&
-               cb < kDescW && nx > 0 && nx < (W - 1) && ny > 0 && ny < (H - 1);
-    };
-    // this wave's rows are j = wv + 4*m; 64 of them (one per lane) per group
-    for (int g0 = wv; g0 < side; g0 += 4 * 64) {
-        const int j = g0 + 4 * lane;
-        const int row = j - radius;
-        int lo = 0, len = 0;
-        if (j < side && row + y > 0 && row + y < H - 1) {
-            // real-arithmetic interval of |c*sa + row*ca| < 2.5 hw and
-            // |c*ca - row*sa| < 2.5 hw, then snapped with the exact test
-            const double lim = (0.5 * kDescW + 0.5) * hw;
-            double clo = (double)max(-radius, 1 - x), chi = (double)min(radius, W - 2 - x);
-            const double ra = row * ca, rs = row * sa;
-            if (sa != 0.0) {
-                const double a1 = (-lim - ra) / sa, a2 = (lim - ra) / sa;
-                clo = fmax(clo, fmin(a1, a2));
-                chi = fmin(chi, fmax(a1, a2));
-            } else if (!(fabs(ra) < lim)) {
-                chi = clo - 1.0;
-            }
-            if (ca != 0.0) {
-                const double b1 = (-lim + rs) / ca, b2 = (lim + rs) / ca;
-                clo = fmax(clo, fmin(b1, b2));
-                chi = fmin(chi, fmax(b1, b2));
-            } else if (!(fabs(rs) < lim)) {
-                chi = clo - 1.0;
-            }
-            if (clo <= chi + 2.0) {
-                lo = (int)ceil(clo);
-                int hi = (int)floor(chi);
-                for (int t = 0; t < 3 && accepted(row, lo - 1); ++t) --lo;
-                for (int t = 0; t < 3 && lo <= hi + 1 && !accepted(row, lo); ++t) ++lo;
-                for (int t = 0; t < 3 && accepted(row, hi + 1); ++t) ++hi;
-                for (int t = 0; t < 3 && hi >= lo && !accepted(row, hi); ++t) --hi;
-                len = hi >= lo ? hi - lo + 1 : 0;
-            }
-        }
-        // inclusive scan of the row lengths across the wave
-        int pre = len;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int t = __shfl_up(pre, off);
-            if (lane >= off) pre += t;
-        }
-        const int total = __builtin_amdgcn_readlane(pre, 63);
-        int cur = 0;  // first row (lane index) whose samples are not all consumed
-        // (row, col) of sample t0 + lane; false past the end. Wave-uniform
-        // call sites only (shuffles); advances the row cursor.
-        auto locate = [&](int t0, int& srow, int& scol) -> bool {
-            const int t = t0 + lane;
-            // row r of sample t: the first r >= cur with pre_r > t
-            int r = cur;
-            int nxt = cur;
-            for (int q = cur; q < 64; ++q) {
-                const int pq = __builtin_amdgcn_readlane(pre, q);
-                if (pq > t0 + 63) break;
-                r += (pq <= t) ? 1 : 0;
-                nxt = q + 1;
-            }
-            const int lo_r = __shfl(lo, r);
-            const int ex_r = __shfl(pre, r) - __shfl(len, r);
-            cur = nxt;
-            srow = g0 + 4 * r - radius;
-            scol = lo_r + (t - ex_r);
-            return t < total;
-        };
-        // The four gradient loads are issued unconditionally (lanes past the
-        // end read pixel (1, 1)): loads under a branch leave the compiler's
-        // wait-count bookkeeping unable to count them, and it then waits for
-        // the prefetched sample before processing the current one
-        auto fetch = [&](bool ok, int srow, int scol, double* v) {
-            const size_t r0 = ok ? (size_t)(srow + y) * W + scol + x : (size_t)W + 1;
-            v[0] = img[r0 + 1];
-            v[1] = img[r0 - 1];
-            v[2] = img[r0 - W];
-            v[3] = img[r0 + W];
-        };
-        // kAhead samples ahead: the next samples' gradient loads are in
-        // flight while the current one is processed
-        constexpr int kAhead = SIFT_DESC_AHEAD;
-        int srow = 0, scol = 0;
-        double cv[4] = {0.0, 0.0, 0.0, 0.0};
-        bool cok = total > 0 && locate(0, srow, scol);
-        fetch(cok, srow, scol, cv);
-        int qrow[kAhead], qcol[kAhead];
-        bool qok[kAhead];
-        double qv[kAhead][4];
-#pragma unroll
-        for (int a = 0; a + 1 < kAhead; ++a) {
-            qrow[a] = qcol[a] = 0;
-            qok[a] = false;
-            if (64 * (a + 1) < total) qok[a] = locate(64 * (a + 1), qrow[a], qcol[a]);
-            fetch(qok[a], qrow[a], qcol[a], qv[a]);
-        }
-        for (int t0 = 0; t0 < total; t0 += 64) {
-            int& nrow = qrow[kAhead - 1];
-            int& ncol = qcol[kAhead - 1];
-            bool& nok = qok[kAhead - 1];
-            nrow = ncol = 0;
-            nok = false;
-            if (t0 + 64 * kAhead < total) nok = locate(t0 + 64 * kAhead, nrow, ncol);
-            fetch(nok, nrow, ncol, qv[kAhead - 1]);
-            if (F32 && cok) {
-                const float fcol = (float)scol, frow = (float)srow;
-                const float row_rot = fmaf(fcol, saf, frow * caf) * ihwf;
-                const float col_rot = fmaf(fcol, caf, -(frow * saf)) * ihwf;
-                const float rb = row_rot + (float)(kDescW / 2 - 0.5);
-                const float cb = col_rot + (float)(kDescW / 2 - 0.5);
-                const float dx = (float)(cv[0] - cv[1]);
-                const float dy = (float)(cv[2] - cv[3]);
-                const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));  // 1 ulp
-                // unwrapped angle: floor/fraction of the bin position are the
-                // reference's after wrapping into [0, 2pi); the bin index is
-                // reduced mod 8 instead (fmods of sift.cpp:667)
-                const float ob = (atan2_f32(dy, dx) - porif) * (float)(kDescBins / kTwoPi);
-                const float wgt =
-                    __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
-                const float m = mag * wgt;
-                const float fbr = floorf(rb), fbc = floorf(cb), fbo = floorf(ob);
-                const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
-                const float fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
-#pragma unroll
-                for (int rq = 0; rq <= 1; ++rq) {
-                    const int ri = br + rq;
-                    if (ri < 0 || ri >= kDescW) continue;
-                    const float vr = m * ((rq == 0) ? 1.0f - fr : fr);
-#pragma unroll
-                    for (int cq = 0; cq <= 1; ++cq) {
-                        const int ci = bc + cq;
-                        if (ci < 0 || ci >= kDescW) continue;
-                        const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
-                        HT* hb = &hw_rep[ri * 32 + ci * 8];
-                        atomicAdd(&hb[bo & 7], (HT)(vc * (1.0f - fo)));
-                        atomicAdd(&hb[(bo + 1) & 7], (HT)(vc * fo));
-                    }
-                }
-            } else if (!F32 && cok) {
-                const double row_rot = div_sum_w(scol * sa + srow * ca, hw, ihw);
-                const double col_rot = div_sum_w(scol * ca - srow * sa, hw, ihw);
-                const double rb = row_rot + kDescW / 2 - 0.5;
-                const double cb = col_rot + kDescW / 2 - 0.5;
-                const double dx = cv[0] - cv[1];
-                const double dy = cv[2] - cv[3];
-                const double mag = sqrt(dx * dx + dy * dy);
-                double ang = atan2(dy, dx);
-                ang -= pori;
-                // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi:
-                // fmod(a, M) = a - trunc(a/M) M is exact and representable,
-                // so one compare-and-subtract reproduces it bit for bit.
-                if (ang >= kTwoPi) ang -= kTwoPi;
-                else if (ang <= -kTwoPi) ang += kTwoPi;
-                ang += kTwoPi;  // rounded, as in the reference
-                if (ang >= kTwoPi) ang -= kTwoPi;
-                if (ang >= kTwoPi) ang -= kTwoPi;
-                const double ob = ang * bins_per_rad;
-                const double wgt = exp(-(row_rot * row_rot + col_rot * col_rot) / denom);
-                const double m = mag * wgt;
-                const int br = (int)floor(rb), bc = (int)floor(cb), bo = (int)floor(ob);
-                const double fr = rb - br, fc = cb - bc, fo = ob - bo;
-#pragma unroll
-                for (int rq = 0; rq <= 1; ++rq) {
-                    const int ri = br + rq;
-                    if (ri < 0 || ri >= kDescW) continue;
-                    const double vr = m * ((rq == 0) ? 1.0 - fr : fr);
-#pragma unroll
-                    for (int cq = 0; cq <= 1; ++cq) {
-                        const int ci = bc + cq;
-                        if (ci < 0 || ci >= kDescW) continue;
-                        const double vc = vr * ((cq == 0) ? 1.0 - fc : fc);
-#pragma unroll
-                        for (int q = 0; q <= 1; ++q) {
-                            const int oi = (bo + q) % kDescBins;
-                            atomicAdd(&hw_rep[ri * 32 + ci * 8 + oi],
-                                      (HT)(vc * ((q == 0) ? 1.0 - fo : fo)));
-                        }
-                    }
-                }
-            }
-            srow = qrow[0];
-            scol = qcol[0];
-            cok = qok[0];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cv[q] = qv[0][q];
-#pragma unroll
-            for (int a = 0; a + 1 < kAhead; ++a) {
-                qrow[a] = qrow[a + 1];
-                qcol[a] = qcol[a + 1];
-                qok[a] = qok[a + 1];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
-            }
-        }
-    }
-    __syncthreads();
-    double v = 0.0;
-    if (tid < 128) {
-#pragma unroll
-        for (int r = 0; r < 4 * kReps; ++r) v += (double)S.hist[r * kDescRepStride + tid];
-    }
-    // L2 normalise, clamp at DESC_MAGNITUDE_THR, renormalise (sift.cpp:576-603)
-    double sq = v * v;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
-    if (lane == 0 && wv < 2) S.red[wv] = sq;
-    __syncthreads();
-    const double ninv = 1.0 / sqrt(S.red[0] + S.red[1]);
-    double cv = v * ninv;
-    if (cv > kMagThr) cv = kMagThr;
-    double sq2 = tid < 128 ? cv * cv : 0.0;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) sq2 += __shfl_xor(sq2, off);
-    if (lane == 0 && wv < 2) S.red[2 + wv] = sq2;
-    __syncthreads();
-    if (tid < 128) {
-        const double inv2 = 1.0 / sqrt(S.red[2] + S.red[3]);
-        const double q = floor(kIntFactor * cv * inv2);
-        int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
-        val = val < 0 ? 0 : (val > 255 ? 255 : val);
-        recs[rec].desc[tid] = (uint8_t)val;
-        if (desc_f32) desc_f32[(size_t)rec * 128 + tid] = (float)(cv * inv2);
-        if (rec < ex.cap) {
-            ex.rec[rec].desc[tid] = (uint8_t)val;
-            if (tid == 0) {
-                sift_kp& r = ex.rec[rec];
-                r.x = kx;
-                r.y = ky;
-                r.octave = o;
-                r.layer = layer;
-                r.size = ksize;
-                r.pori = pori;
-                ex.side[rec] = rside;
-            }
-        }
-    }
-}
 
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const unsigned long long u = __double_as_longlong(v);
@@ -2104,335 +1700,6 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             }
         }
         wave_sync();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_descriptor_wave (desc_mode 1, the default): one WAVEFRONT per record
-// (sift.cpp:610-682), four independent waves per workgroup pulling records
-// from the work counter; no workgroup barrier anywhere.
-//
-// Per-record cost was dominated by work every wave of the 256-thread
-// version repeated (record setup with f64 sin/cos, the f64 row-interval
-// solve with exact snapping, histogram zero/reduce/normalise): ~1150 VALU
-// instructions per wave per record against ~1100 for the samples
-// themselves (r02 SQ counters). Here a record's setup runs once, and:
-//  * The sample set is enumerated as an f32 SUPERSET of the reference's
-//    rotated box (row intervals widened by 0.01 column). No exact test is
-//    needed: a sample's trilinear weights vanish continuously at the box
-//    edges (row_bin -> -1 puts weight fr -> 0 on row 0 and the rest on the
-//    skipped row -1; row_bin -> 4 puts 1 - fr -> 0 on row 3), so a sample
-//    just outside contributes exactly nothing (its cells are skipped) and
-//    one just inside contributes ~1e-7 of its magnitude — the same order as
-//    the f32 sample math itself (contract: 1e-4 on the floats).
-//  * Sample math as describe<1> (f32, f64 histograms); the integer bounds
-//    (radius, image border) are exact.
-//  * kDescWReps replica-interleaved f64 copies of the 4x4x8 histogram per
-//    wave; the 128 bins are reduced two per lane (bins l and l + 64), the
-//    two normalisation sums are in-wave reductions.
-// A wave's LDS instructions execute in order, so zeroing -> accumulation
-// -> reduction -> next record's zeroing needs only compiler ordering
-// (wave_sync).
-// ---------------------------------------------------------------------------
-#ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
-#define SIFT_DESCW_REPS 16
-#endif
-#ifndef SIFT_DESCW_OCC  // min workgroups per CU (16 replicas: 64 KB LDS each)
-#define SIFT_DESCW_OCC (SIFT_DESCW_REPS >= 16 ? 2 : 5)
-#endif
-#ifndef SIFT_DESCW_WALK
-#define SIFT_DESCW_WALK 0
-#endif
-#ifndef SIFT_DESCW_AHEAD
-#define SIFT_DESCW_AHEAD 1
-#endif
-constexpr int kDescWReps = SIFT_DESCW_REPS;
-static_assert(kDescWReps >= 1 && kDescWReps <= 16 && (kDescWReps & (kDescWReps - 1)) == 0,
-              "replicas: a power of two <= 16");
-// Replica-interleaved layout: bin i of replica r at hist[i * kDescWReps + r],
-// r = lane % kDescWReps. ds_add_f64 serves 16 lanes per LDS cycle over 32
-// banks (bank = dword address mod 32); a lane's bank pair is then
-// 2 (i * kDescWReps + r) mod 32, so with 16 replicas every lane of a group
-// owns its bank pair whatever bins the samples hit (conflict-free), with 8
-// two lanes share a replica and collide only on bins of equal parity. (A
-// replica-major layout, r * stride + i, leaves the bank to the bin: the
-// atomics measured ~1 extra LDS cycle per LDS cycle, lane % 4 or % 16 alike.)
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-
-__global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
-    const PyrTable* __restrict__ pt, DevParams P, sift_kp* __restrict__ recs,
-    const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
-    const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
-    unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kDescWReps];
-    set_job_prio(pt->jp, 0);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double* const hist = hist_all + wv * 128 * kDescWReps;
-    double* const rep = hist + (lane & (kDescWReps - 1));  // bin i at rep[i * kDescWReps]
-    const unsigned n = min(*n_rec, cap_rec);
-    const unsigned k0 = min(*rec_begin, n);
-    // the launch's record range is fixed before it starts (orientation has
-    // completed); the host reads it after the chain's completion event
-    if (ex.cnt && blockIdx.x == 0 && threadIdx.x == 0) {
-        ex.cnt[0] = k0;
-        ex.cnt[1] = n;
-    }
-    constexpr float kHalfW = (float)(kDescW / 2 - 0.5);  // row_bin = row_rot + 1.5
-    const float wscale = (float)(-1.4426950408889634 / (0.5 * kDescW * kDescW));
-    for (;;) {
-        unsigned claim = 0;
-        if (lane == 0) claim = atomicAdd(work, 1u);
-        const unsigned k = k0 + __builtin_amdgcn_readfirstlane(claim);
-        if (k >= n) break;
-        // ---- record setup (wave-uniform)
-        const sift_kp& R = recs[k];
-        const double kx = R.x, ky = R.y, ksize = R.size, pori = R.pori;
-        const int o = R.octave, layer = R.layer;
-        const RecSide rside = rec_side[k];
-        gdouble* img = gbl(plane(pt, rside.img, o, layer));
-        const int W = pt->w[o], H = pt->h[o];
-        const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
-        const int x = (int)(kx * inv);
-        const int y = (int)(ky * inv);
-        const double hw = P.desc_scale_factor * (ksize * inv);
-        const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
-        const double diag = sqrt((double)(W * W + H * H));
-        const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
-        const int side = 2 * radius + 1;
-        float saf, caf;
-        sincosf((float)pori, &saf, &caf);
-        const float ihwf = (float)(1.0 / hw);
-        const float porif = (float)pori;
-        // |row_rot| < 2.5 and |col_rot| < 2.5, in units of hw
-        const float limf = (float)((0.5 * kDescW + 0.5) * hw);
-        for (int i = lane; i < 64 * kDescWReps; i += 64)
-            reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
-        wave_sync();
-        // ---- rows in groups of 64 (lane = row), samples 64 at a time
-        for (int g0 = 0; g0 < side; g0 += 64) {
-            const int row = g0 + lane - radius;
-            int lo = 0, len = 0;
-            if (g0 + lane < side && row + y > 0 && row + y < H - 1) {
-                const float fr = (float)row, ra = fr * caf, rs = fr * saf;
-                float clo = (float)max(-radius, 1 - x), chi = (float)min(radius, W - 2 - x);
-                // |c sa + r ca| < lim and |c ca - r sa| < lim, widened by 0.01
-                // column (f32 rounding of the bounds is far below that)
-                if (fabsf(saf) > 1e-6f) {
-                    const float is = 1.0f / saf;
-                    const float a1 = (-limf - ra) * is, a2 = (limf - ra) * is;
-                    clo = fmaxf(clo, fminf(a1, a2) - 0.01f);
-                    chi = fminf(chi, fmaxf(a1, a2) + 0.01f);
-                } else if (!(fabsf(ra) < limf + 0.01f)) {
-                    chi = clo - 1.0f;
-                }
-                if (fabsf(caf) > 1e-6f) {
-                    const float ic = 1.0f / caf;
-                    const float b1 = (-limf + rs) * ic, b2 = (limf + rs) * ic;
-                    clo = fmaxf(clo, fminf(b1, b2) - 0.01f);
-                    chi = fminf(chi, fmaxf(b1, b2) + 0.01f);
-                } else if (!(fabsf(rs) < limf + 0.01f)) {
-                    chi = clo - 1.0f;
-                }
-                lo = (int)ceilf(clo);
-                const int hi = (int)floorf(chi);
-                len = hi >= lo ? hi - lo + 1 : 0;
-            }
-            int pre = len;  // inclusive scan of the row lengths
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int t = __shfl_up(pre, off);
-                if (lane >= off) pre += t;
-            }
-            const int total = __builtin_amdgcn_readlane(pre, 63);
-            // (row, col) of sample t0 + lane; false past the end. Its row r
-            // is the number of rows whose inclusive prefix is <= t: a
-            // branch-free binary search over the 64 prefixes (the scalar
-            // walk over the rows a block touches cost ~20 SALU per block)
-#if SIFT_DESCW_WALK
-            int cur = 0;  // A/B: the scalar walk
-#endif
-            auto locate = [&](int t0, int& srow, int& scol) -> bool {
-                const int t = t0 + lane;
-#if SIFT_DESCW_WALK
-                int r = cur, nxt = cur;
-                for (int q = cur; q < 64; ++q) {
-                    const int pq = __builtin_amdgcn_readlane(pre, q);
-                    if (pq > t0 + 63) break;
-                    r += (pq <= t) ? 1 : 0;
-                    nxt = q + 1;
-                }
-                cur = nxt;
-#else
-                int r = 0;
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (__shfl(pre, r + step - 1) <= t) r += step;
-#endif
-                const int lo_r = __shfl(lo, r);
-                const int ex_r = __shfl(pre, r) - __shfl(len, r);
-                srow = g0 + r - radius;
-                scol = lo_r + (t - ex_r);
-                return t < total;
-            };
-            // gradient loads issued unconditionally (see describe's fetch)
-            auto fetch = [&](bool ok, int srow, int scol, double* v) {
-                const size_t r0 = ok ? (size_t)(srow + y) * W + scol + x : (size_t)W + 1;
-                v[0] = img[r0 + 1];
-                v[1] = img[r0 - 1];
-                v[2] = img[r0 - W];
-                v[3] = img[r0 + W];
-            };
-            // kAhead blocks of 64 samples whose gradient loads are in flight
-            // while the current block is processed
-            constexpr int kAhead = SIFT_DESCW_AHEAD;
-            int srow = 0, scol = 0, qrow[kAhead], qcol[kAhead];
-            bool qok[kAhead];
-            double cv[4] = {0.0, 0.0, 0.0, 0.0}, qv[kAhead][4];
-            bool cok = total > 0 && locate(0, srow, scol);
-            fetch(cok, srow, scol, cv);
-#pragma unroll
-            for (int a = 0; a + 1 < kAhead; ++a) {
-                qrow[a] = qcol[a] = 0;
-                qok[a] = 64 * (a + 1) < total && locate(64 * (a + 1), qrow[a], qcol[a]);
-                fetch(qok[a], qrow[a], qcol[a], qv[a]);
-            }
-            for (int t0 = 0; t0 < total; t0 += 64) {
-                {
-                    int& nrow = qrow[kAhead - 1];
-                    int& ncol = qcol[kAhead - 1];
-                    nrow = ncol = 0;
-                    qok[kAhead - 1] =
-                        t0 + 64 * kAhead < total && locate(t0 + 64 * kAhead, nrow, ncol);
-                    fetch(qok[kAhead - 1], nrow, ncol, qv[kAhead - 1]);
-                }
-                if (cok) {
-                    const float fcol = (float)scol, frow = (float)srow;
-                    const float row_rot = fmaf(fcol, saf, frow * caf) * ihwf;
-                    const float col_rot = fmaf(fcol, caf, -(frow * saf)) * ihwf;
-                    const float rb = row_rot + kHalfW;
-                    const float cb = col_rot + kHalfW;
-                    const float dx = (float)(cv[0] - cv[1]);
-                    const float dy = (float)(cv[2] - cv[3]);
-                    const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
-                    const float ob = (atan2_f32(dy, dx) - porif) * (float)(kDescBins / kTwoPi);
-                    const float wgt =
-                        __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
-                    const float m = mag * wgt;
-                    const float fbr = floorf(rb), fbc = floorf(cb), fbo = floorf(ob);
-                    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
-                    const float fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
-#pragma unroll
-                    for (int rq = 0; rq <= 1; ++rq) {
-                        const int ri = br + rq;
-                        if ((unsigned)ri >= (unsigned)kDescW) continue;
-                        const float vr = m * ((rq == 0) ? 1.0f - fr : fr);
-#pragma unroll
-                        for (int cq = 0; cq <= 1; ++cq) {
-                            const int ci = bc + cq;
-                            if ((unsigned)ci >= (unsigned)kDescW) continue;
-                            const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
-                            double* hb = &rep[(ri * 32 + ci * 8) * kDescWReps];
-                            atomicAdd(&hb[(bo & 7) * kDescWReps], (double)(vc * (1.0f - fo)));
-                            atomicAdd(&hb[((bo + 1) & 7) * kDescWReps], (double)(vc * fo));
-                        }
-                    }
-                }
-                srow = qrow[0];
-                scol = qcol[0];
-                cok = qok[0];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) cv[q] = qv[0][q];
-#pragma unroll
-                for (int a = 0; a + 1 < kAhead; ++a) {
-                    qrow[a] = qrow[a + 1];
-                    qcol[a] = qcol[a + 1];
-                    qok[a] = qok[a + 1];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
-                }
-            }
-        }
-        wave_sync();
-        // ---- reduce the replicas (bins lane, lane + 64), normalise, clamp,
-        // renormalise, quantise (sift.cpp:576-603)
-        double v0 = 0.0, v1 = 0.0;
-#pragma unroll
-        for (int q = 0; q < kDescWReps; ++q) {
-            // fixed order per bin, rotated by lane so the 16 lanes of a read
-            // group start on different bank pairs
-            const int r = (q + lane) & (kDescWReps - 1);
-            v0 += hist[lane * kDescWReps + r];
-            v1 += hist[(lane + 64) * kDescWReps + r];
-        }
-        const double ninv = 1.0 / sqrt(wave_sum_f64(v0 * v0 + v1 * v1));
-        double c0 = v0 * ninv, c1 = v1 * ninv;
-        if (c0 > kMagThr) c0 = kMagThr;
-        if (c1 > kMagThr) c1 = kMagThr;
-        const double inv2 = 1.0 / sqrt(wave_sum_f64(c0 * c0 + c1 * c1));
-        auto quant = [&](double c) -> uint8_t {
-            const double q = floor(kIntFactor * c * inv2);
-            int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
-            return (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
-        };
-        const uint8_t u0 = quant(c0), u1 = quant(c1);
-        recs[k].desc[lane] = u0;
-        recs[k].desc[lane + 64] = u1;
-        if (desc_f32) {
-            desc_f32[(size_t)k * 128 + lane] = (float)(c0 * inv2);
-            desc_f32[(size_t)k * 128 + lane + 64] = (float)(c1 * inv2);
-        }
-        if (k < ex.cap) {
-            ex.rec[k].desc[lane] = u0;
-            ex.rec[k].desc[lane + 64] = u1;
-            if (lane == 0) {
-                sift_kp& r = ex.rec[k];
-                r.x = kx;
-                r.y = ky;
-                r.octave = o;
-                r.layer = layer;
-                r.size = ksize;
-                r.pori = pori;
-                ex.side[k] = rside;
-            }
-        }
-        wave_sync();
-    }
-}
-
-// Descriptors of records [*rec_begin, *n_rec), one workgroup per record
-// from a work counter; workgroup 0 publishes the range.
-template <int MODE>
-__global__ __launch_bounds__(256, MODE == 0 ? 3 : (MODE == 1 ? SIFT_DESC_OCC : 4)) void k_descriptor(const PyrTable* __restrict__ pt, DevParams P,
-                                                    sift_kp* __restrict__ recs,
-                                                    const RecSide* __restrict__ rec_side,
-                                                    const unsigned* __restrict__ rec_begin,
-                                                    const unsigned* __restrict__ n_rec,
-                                                    unsigned cap_rec, float* __restrict__ desc_f32,
-                                                    unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ DescLdsT<MODE> S;
-    const int tid = threadIdx.x;
-    const unsigned n = min(*n_rec, cap_rec);
-    const unsigned k0 = min(*rec_begin, n);
-    // the launch's record range is fixed before it starts (orientation has
-    // completed); the host reads it after the chain's completion event
-    if (ex.cnt && blockIdx.x == 0 && tid == 0) {
-        ex.cnt[0] = k0;
-        ex.cnt[1] = n;
-    }
-    for (;;) {
-        if (tid == 0) S.k = k0 + atomicAdd(work, 1u);
-        __syncthreads();
-        const unsigned k = S.k;
-        if (k >= n) break;
-        const double* hdr = reinterpret_cast<const double*>(&recs[k]);
-        describe<MODE>(S, pt, P, recs, k, hdr[0], hdr[1], reinterpret_cast<const int*>(hdr)[4],
-                 reinterpret_cast<const int*>(hdr)[5], hdr[3], hdr[4], rec_side[k], desc_f32, ex);
-        __syncthreads();
     }
 }
 
@@ -2886,26 +2153,6 @@ hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* 
     const size_t lds = (size_t)(4 * kOriReps * (P.num_bins + 2) + kOriTab) * sizeof(double);
     hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), lds, s, d_pt, P, raw, raw_begin, n_raw,
                        cap_raw, recs, rec_side, n_rec, cap_rec, work);
-    return hipGetLastError();
-}
-
-hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
-                             const RecSide* rec_side, const unsigned* rec_begin,
-                             const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
-                             unsigned* work, const ExportSink& ex, unsigned wgs,
-                             int mode, hipStream_t s) {
-    unsigned blocks = wgs;  // persistent: workgroups pull records
-    if (mode == 1) {  // four waves per workgroup, a record per wave
-        blocks = std::min<unsigned>(blocks, cap_rec > 0 ? (cap_rec + 3) / 4 : 1);
-        hipLaunchKernelGGL(k_descriptor_wave, dim3(blocks), dim3(256), 0, s, d_pt, P, recs,
-                           rec_side, rec_begin, n_rec, cap_rec, desc_f32, work, ex);
-        return hipGetLastError();
-    }
-    if (blocks > cap_rec) blocks = cap_rec > 0 ? cap_rec : 1;
-    // 3: the 256-threads-per-record f32 variant (A/B against mode 1)
-    auto kern = mode == 0 ? k_descriptor<0> : mode == 3 ? k_descriptor<1> : k_descriptor<2>;
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_side,
-                       rec_begin, n_rec, cap_rec, desc_f32, work, ex);
     return hipGetLastError();
 }
 
