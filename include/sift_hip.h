@@ -193,7 +193,9 @@ int sift_hip_fetch_device_async(sift_ctx* ctx, int ticket, void* d_out, size_t c
  * hdr_rows header rows of 168 bytes. Every slot whose records' wrapping word
  * sum differs from the sum of its checksums (or whose n exceeds cap_rows)
  * adds 1 to *d_bad (device memory). Enqueued on `stream` (default: the
- * context's), no host wait. */
+ * context's), no host wait. Calls of one context share its scratch and run
+ * in call order on the device, whatever their streams (each waits for the
+ * previous call's completion event). */
 int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_t slot_bytes,
                           int hdr_rows, int count_word, int sum_word, int n_sum_words,
                           size_t cap_rows, uint64_t* d_bad, void* stream);

@@ -100,27 +100,38 @@ public:
             for (unsigned t = 0; t < n_tasks; ++t) fn(t);
             return;
         }
+        unsigned gen;
         {
             std::lock_guard<std::mutex> g(m_);
+            gen = ++gen_;
             fn_ = &fn;
-            n_tasks_.store(n_tasks);
-            next_.store(0);
+            n_tasks_ = n_tasks;
             pending_ = n_tasks;
-            ++gen_;
+            claim_.store((uint64_t)gen << 32);
         }
         cv_.notify_all();
-        work();
+        work(gen, n_tasks, &fn);
         std::unique_lock<std::mutex> g(m_);
         done_cv_.wait(g, [this] { return pending_ == 0; });
         fn_ = nullptr;
     }
 
 private:
-    void work() {
+    // Claims carry the generation: claim_ = gen << 32 | next task index, and
+    // a task is taken only by a compare-exchange that still sees the
+    // worker's own generation. A worker that wakes late (its generation
+    // already finished and the next one posted) fails the exchange and
+    // returns, so it never runs, or counts down, another generation's task.
+    void work(unsigned gen, unsigned n_tasks, const std::function<void(unsigned)>* fn) {
         for (;;) {
-            const unsigned t = next_.fetch_add(1);
-            if (t >= n_tasks_) return;
-            (*fn_)(t);
+            uint64_t c = claim_.load();
+            unsigned t;
+            do {
+                if ((unsigned)(c >> 32) != gen) return;
+                t = (unsigned)c;
+                if (t >= n_tasks) return;
+            } while (!claim_.compare_exchange_weak(c, c + 1));
+            (*fn)(t);
             std::lock_guard<std::mutex> g(m_);
             if (--pending_ == 0) done_cv_.notify_all();
         }
@@ -128,21 +139,25 @@ private:
     void loop() {
         unsigned seen = 0;
         for (;;) {
+            unsigned gen, n;
+            const std::function<void(unsigned)>* fn;
             {
                 std::unique_lock<std::mutex> g(m_);
                 cv_.wait(g, [&] { return stop_ || gen_ != seen; });
                 if (stop_) return;
-                seen = gen_;
+                seen = gen = gen_;
+                n = n_tasks_;
+                fn = fn_;
             }
-            work();
+            work(gen, n, fn);
         }
     }
     std::vector<std::thread> workers_;
     std::mutex m_, run_m_;
     std::condition_variable cv_, done_cv_;
-    const std::function<void(unsigned)>* fn_ = nullptr;
-    unsigned pending_ = 0, gen_ = 0;
-    std::atomic<unsigned> n_tasks_{0}, next_{0};
+    const std::function<void(unsigned)>* fn_ = nullptr;  // guarded by m_
+    unsigned pending_ = 0, gen_ = 0, n_tasks_ = 0;       // guarded by m_
+    std::atomic<uint64_t> claim_{0};
     bool stop_ = false;
 };
 

@@ -254,6 +254,7 @@ struct Slot {
     // completed before the slot is reused (sift_hip_fetch_device_async)
     hipEvent_t gather_ev = nullptr;
     bool gather_pending = false;
+    bool job_done_enqueued = false;  // this job's k_job_done is on a stream
     sift_counts counts{};
     clk::time_point t_submit;
     double t_host[6] = {0, 0, 0, 0, 0, 0};  // [5]: blocked on device events in finalize
@@ -337,7 +338,10 @@ struct sift_ctx {
     // jobs (k_job_done at the end of every job)
     bool age_prio = true;
     unsigned* d_done = nullptr;
+    unsigned prio_seq = 0;  // jobs whose k_job_done was enqueued (JobPrio.ticket)
     DevBuf<unsigned long long> verify_acc;  // sift_hip_verify_slots: per-slot sums
+    hipEvent_t verify_ev = nullptr;         // the last verify_slots call's end
+    bool verify_used = false;
     int pipe_hint = 0;
     int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     // SIFT_DESC_MODE: 0 = k_descriptor_split, f64 sample math (default, the
@@ -922,7 +926,10 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         SIFT_HIP_TRY(hipEventRecord(jd, sD));
         SIFT_HIP_TRY(hipStreamWaitEvent(sC, jd, 0));
     }
-    if (s.taps_init.jp.done) SIFT_HIP_TRY(launch_job_done(ctx->d_done, sC));
+    if (s.taps_init.jp.done) {
+        SIFT_HIP_TRY(launch_job_done(ctx->d_done, sC));
+        s.job_done_enqueued = true;
+    }
     SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                 hipMemcpyDeviceToHost, sC));
     SIFT_HIP_TRY(record_event(s, s.done_ev, sC));
@@ -1288,12 +1295,17 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     if (!sp) return SIFT_ERR_STATE;  // SIFT_MAX_INFLIGHT jobs already in flight
     Slot& s = *sp;
     // an async device fetch may still read this slot's records: the new
-    // job's streams wait for it on the device (below), not the host
+    // job's streams wait for it on the device (below), not the host. The
+    // flag is cleared only once those waits are enqueued, so a submit that
+    // fails before them leaves it for the next one.
     const bool gather_wait = s.gather_pending;
-    s.gather_pending = false;
     int st = host_plan(p, w, h, c, &s.g, &s.taps_init, s.taps, &s.dp);
     if (st != SIFT_OK) return st;
-    const JobPrio jp{(ctx->age_prio && !ctx->graphs) ? ctx->d_done : nullptr, ctx->next_ticket, 0};
+    // age rank (JobPrio): jobs are numbered by prio_seq, which advances only
+    // when a job's k_job_done was enqueued (the job will count in d_done);
+    // both counters wrap together modulo 2^32
+    const JobPrio jp{(ctx->age_prio && !ctx->graphs) ? ctx->d_done : nullptr,
+                     (int)(ctx->prio_seq + 1u), 0};
     s.taps_init.jp = jp;
     for (BlurTaps& t : s.taps) t.jp = jp;
     SIFT_HIP_TRY(hipSetDevice(ctx->device));
@@ -1384,11 +1396,18 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
         for (int i = 0; i < 4; ++i) {
             bool dup = false;
             for (int j = 0; j < i; ++j) dup |= js[j] == js[i];
-            if (!dup) SIFT_HIP_TRY(hipStreamWaitEvent(js[i], s.gather_ev, 0));
+            if (!dup && hipStreamWaitEvent(js[i], s.gather_ev, 0) != hipSuccess) {
+                s.state = kFree;
+                s.ticket = -1;
+                return SIFT_ERR_HIP;
+            }
         }
+        s.gather_pending = false;
     }
     s.state = kSubmitted;
+    s.job_done_enqueued = false;
     st = enqueue_job_graph(ctx, s, images, kind);
+    if (s.job_done_enqueued) ++ctx->prio_seq;
     if (st != SIFT_OK) {
         abandon(ctx, s);
         return st;
@@ -1608,6 +1627,10 @@ int sift_hip_destroy(sift_ctx* ctx) {
     }
     for (int k = 2 * kPairs; k < kSlots; ++k)
         if (ctx->pool[k]) (void)hipStreamDestroy(ctx->pool[k]);
+    if (ctx->verify_ev) {
+        (void)hipEventSynchronize(ctx->verify_ev);
+        (void)hipEventDestroy(ctx->verify_ev);
+    }
     ctx->verify_acc.release();
     if (ctx->d_done) (void)hipFree(ctx->d_done);
     delete ctx;
@@ -1690,11 +1713,22 @@ int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_
         return SIFT_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    if (ctx->verify_acc.ensure((size_t)std::max(n_slots, 1)) != SIFT_OK) return SIFT_ERR_NOMEM;
+    // every call shares the context's accumulator scratch: calls are chained
+    // on the device (each waits for the previous one's event, whatever its
+    // stream), and the scratch is regrown only after the last call finished
+    if (!ctx->verify_ev)
+        SIFT_HIP_TRY(hipEventCreateWithFlags(&ctx->verify_ev, hipEventDisableTiming));
+    const size_t need = (size_t)std::max(n_slots, 1);
+    if (ctx->verify_acc.cap < need && ctx->verify_used)
+        SIFT_HIP_TRY(hipEventSynchronize(ctx->verify_ev));
+    if (ctx->verify_acc.ensure(need) != SIFT_OK) return SIFT_ERR_NOMEM;
+    if (ctx->verify_used) SIFT_HIP_TRY(hipStreamWaitEvent(st, ctx->verify_ev, 0));
     SIFT_HIP_TRY(launch_verify_slots(d_slots, n_slots, slot_bytes, hdr_rows, count_word, sum_word,
                                      n_sum_words, cap_rows,
                                      reinterpret_cast<unsigned long long*>(d_bad),
                                      ctx->verify_acc.p, st));
+    SIFT_HIP_TRY(hipEventRecord(ctx->verify_ev, st));
+    ctx->verify_used = true;
     return SIFT_OK;
 }
 

@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
     unsigned* __restrict__ work, ExportSink ex) {
     __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kSplitReps];
-    __shared__ double atab[17];
+    __shared__ double2 atab[17];
     __shared__ unsigned next_k;
     set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;

@@ -37,7 +37,7 @@ __device__ __forceinline__ void set_job_prio(const JobPrio& jp, int base) {
     if (jp.done) {
         const int done = (int)__hip_atomic_load(jp.done, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-        const int rank = jp.ticket - 1 - done;
+        const int rank = (int)((unsigned)jp.ticket - 1u - (unsigned)done);  // mod 2^32
         p += rank <= 0 ? SIFT_AGE_BOOST0 : (rank == 1 ? SIFT_AGE_BOOST1 : 0);
     }
     switch (p < 3 ? p : 3) {

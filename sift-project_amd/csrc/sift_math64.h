@@ -22,7 +22,7 @@ namespace {
 //    c = k/16 nearest a (picked from an f32 estimate), atan(a) = atan(c) +
 //    atan(u) with u = (min - c max) / (max + c min), |u| <= 1/32 + 1e-7, one
 //    Newton-refined f64 division and atan(u) through u^11 (next term < 1e-19
-//    relative); quadrant fix-ups with double-double pi/2 and pi. Error about
+//    relative) added to atan(c) as a double-double; quadrant fix-ups with double-double pi/2 and pi. Error about
 //    1 ulp, against glibc's correctly rounded-in-most-cases atan2;
 //  * exp_f64: 2^k exp(r), k = rint(x log2 e), r by Cody-Waite (fdlibm's split
 //    of ln 2), exp(r) by its Taylor series through r^13 (|r| <= 0.347, next
@@ -31,13 +31,27 @@ namespace {
 // tests/test_gpu_math64.py checks all three against the device's own
 // correctly rounded sqrt and ocml atan2 / exp on millions of arguments.
 // ---------------------------------------------------------------------------
-// atan(k/16), k = 0..16, correctly rounded (tools/gen_atan_table.py)
-__constant__ double kAtanTab[17] = {
-    0x0.0p+0,               0x1.ff55bb72cfdeap-5, 0x1.fd5ba9aac2f6ep-4, 0x1.7b97b4bce5b02p-3,
-    0x1.f5b75f92c80ddp-3, 0x1.362773707ebccp-2, 0x1.6f61941e4def1p-2, 0x1.a64eec3cc23fdp-2,
-    0x1.dac670561bb4fp-2, 0x1.0657e94db30d0p-1, 0x1.1e00babdefeb4p-1, 0x1.345f01cce37bbp-1,
-    0x1.4978fa3269ee1p-1, 0x1.5d58987169b18p-1, 0x1.700a7c5784634p-1, 0x1.819d0b7158a4dp-1,
-    0x1.921fb54442d18p-1};
+// atan(k/16), k = 0..16, as double-double pairs (hi = correctly rounded,
+// lo = the remainder rounded; tools/gen_atan_table.py)
+__constant__ double2 kAtanTab[17] = {
+    {0x0.0p+0, 0x0.0p+0},
+    {0x1.ff55bb72cfdeap-5, -0x1.c934d86d23f1dp-60},
+    {0x1.fd5ba9aac2f6ep-4, -0x1.cd37686760c17p-59},
+    {0x1.7b97b4bce5b02p-3, 0x1.347b0b4f881cap-58},
+    {0x1.f5b75f92c80ddp-3, 0x1.8ab6e3cf7afbdp-57},
+    {0x1.362773707ebccp-2, -0x1.963a544b672d8p-57},
+    {0x1.6f61941e4def1p-2, -0x1.c63aae6f6e918p-56},
+    {0x1.a64eec3cc23fdp-2, -0x1.24dec1b50b7ffp-56},
+    {0x1.dac670561bb4fp-2, 0x1.a2b7f222f65e2p-56},
+    {0x1.0657e94db30d0p-1, -0x1.d5b495f6349e6p-56},
+    {0x1.1e00babdefeb4p-1, -0x1.928df287a668fp-58},
+    {0x1.345f01cce37bbp-1, 0x1.1021137c71102p-55},
+    {0x1.4978fa3269ee1p-1, 0x1.2419a87f2a458p-56},
+    {0x1.5d58987169b18p-1, 0x1.0028e4bc5e7cap-57},
+    {0x1.700a7c5784634p-1, -0x1.8c34d25aadef6p-56},
+    {0x1.819d0b7158a4dp-1, -0x1.bf76229d3b917p-56},
+    {0x1.921fb54442d18p-1, 0x1.1a62633145c07p-55},
+};
 
 __device__ __forceinline__ double sqrt_f64(double s) {
     const double y = __builtin_amdgcn_rsq(s);
@@ -53,7 +67,7 @@ __device__ __forceinline__ double sqrt_f64(double s) {
 }
 
 // atan2(y, x); `tab` = kAtanTab staged in LDS
-__device__ __forceinline__ double atan2_f64(double y, double x, const double* tab) {
+__device__ __forceinline__ double atan2_f64(double y, double x, const double2* tab) {
     const double ax = fabs(x), ay = fabs(y);
     const bool swap = ay > ax;
     const double mx = swap ? ay : ax, mn = swap ? ax : ay;
@@ -74,7 +88,8 @@ __device__ __forceinline__ double atan2_f64(double y, double x, const double* ta
     p = __builtin_fma(t, p, -1.0 / 7.0);
     p = __builtin_fma(t, p, 1.0 / 5.0);
     p = __builtin_fma(t, p, -1.0 / 3.0);
-    double th = tab[(int)kf] + __builtin_fma(u * t, p, u);
+    const double2 ck = tab[(int)kf];
+    double th = ck.x + (__builtin_fma(u * t, p, u) + ck.y);
     if (swap) th = (0x1.921fb54442d18p+0 - th) + 0x1.1a62633145c07p-54;  // pi/2 - th
     if (x < 0.0) th = (0x1.921fb54442d18p+1 - th) + 0x1.1a62633145c07p-53;  // pi - th
     if (!(mx > 0.0)) th = __builtin_signbit(x) ? 0x1.921fb54442d18p+1 : 0.0;

@@ -225,6 +225,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
+SIFT_ERR_ARG = -1  # include/sift_hip.h
+
+
 def _check(st: int) -> None:
     if st != 0:
         msg = load_library().sift_hip_strerror(st).decode()
@@ -333,8 +336,8 @@ class Context:
         """Final records of a job written to device memory (image-major, cap
         records available); per-image counts. Releases the job."""
         counts = self.wait(ticket)
-        _check(self.lib.sift_hip_fetch_device(self._ctx, ticket, ctypes.c_void_p(dev_ptr), cap))
-        del self._jobs[ticket]
+        self._release_after(ticket, self.lib.sift_hip_fetch_device(
+            self._ctx, ticket, ctypes.c_void_p(dev_ptr), cap))
         return counts
 
     def fetch_device_async(self, ticket: int, dev_ptr: int, cap: int, stream: int = 0,
@@ -345,11 +348,18 @@ class Context:
         64-bit word sum goes to device memory at checksum_ptr. Releases the
         job; returns per-image counts."""
         counts = self.wait(ticket)
-        _check(self.lib.sift_hip_fetch_device_async(
+        self._release_after(ticket, self.lib.sift_hip_fetch_device_async(
             self._ctx, ticket, ctypes.c_void_p(dev_ptr), cap, ctypes.c_void_p(stream or None),
             ctypes.c_void_p(checksum_ptr or None)))
-        del self._jobs[ticket]
         return counts
+
+    def _release_after(self, ticket: int, st: int) -> None:
+        """Status of a device fetch: the library keeps the job only when
+        the caller's capacity was too small (SIFT_ERR_ARG, the job stays
+        fetchable); any other outcome released it, so the ticket goes too."""
+        if st != SIFT_ERR_ARG:
+            del self._jobs[ticket]
+        _check(st)
 
     def verify_slots(self, slots_ptr: int, n_slots: int, slot_bytes: int, hdr_rows: int,
                      count_word: int, sum_word: int, n_sum_words: int, cap_rows: int,

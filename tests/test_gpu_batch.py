@@ -329,3 +329,33 @@ def test_gpu_graph_replay_equals_eager():
     finally:
         graphed.close()
         eager.close()
+
+
+def test_gpu_async_fetch_then_failed_submit_on_same_slot(gpu_ctx):
+    """a submit that fails (bad parameters) on a slot whose async
+    device gather is still pending must leave the pending flag for the next
+    submit, whose streams then wait for the gather before overwriting the
+    slot's records. With MAX_INFLIGHT - 1 jobs in flight the freed slot is
+    the only free one, so both submits land on it."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    w, h = 640, 480
+    img = synth_image(w, h, 1, seed=314)
+    other = synth_image(w, h, 1, seed=315)
+    ref, _ = gpu_ctx.detect(img)
+    ref_other, _ = gpu_ctx.detect(other)
+    n = len(ref)
+    tickets = [gpu_ctx.submit([img], INPUT_F64_HOST, w, h, 1) for _ in range(MAX_INFLIGHT)]
+    out = torch.full((n + 3, 168), 0xCD, dtype=torch.uint8, device=dev)
+    gpu_ctx.fetch_device_async(tickets[0], out.data_ptr(), n + 3,
+                               torch.cuda.current_stream().cuda_stream)
+    with pytest.raises(RuntimeError, match="parameter"):
+        gpu_ctx.submit([img], INPUT_F64_HOST, w, h, 1, SiftParams(intervals=0))
+    t_new = gpu_ctx.submit([other], INPUT_F64_HOST, w, h, 1)
+    torch.cuda.synchronize()
+    assert out[:n].cpu().numpy().tobytes() == ref.tobytes()
+    assert bool((out[n:] == 0xCD).all())
+    _assert_same_records(gpu_ctx.fetch(t_new)[0][0], ref_other)
+    for t in tickets[1:]:
+        _assert_same_records(gpu_ctx.fetch(t)[0][0], ref)

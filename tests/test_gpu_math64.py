@@ -32,4 +32,4 @@ def test_gpu_math64_accuracy():
     assert res["sqrt"]["ulp_max_dev"] == 0 and res["sqrt"]["ulp_max_glibc"] == 0
     for fn in ("atan2", "exp"):
         assert res[fn]["ulp_max_glibc"] <= 2, (fn, res[fn])
-        assert res[fn]["diff_frac_glibc"] < 0.05, (fn, res[fn])
+        assert res[fn]["diff_frac_glibc"] < 0.25, (fn, res[fn])

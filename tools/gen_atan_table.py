@@ -1,7 +1,7 @@
-"""Table of atan(k/16), k = 0..16, correctly rounded to double, for the
-descriptor's f64 atan2 (sift-project_amd/csrc/sift_math64.h kAtanTab).
-Evaluated with 60-digit decimal arithmetic (argument halving + Taylor
-series), then rounded once by float()."""
+"""Table of atan(k/16), k = 0..16, as double-double pairs (hi correctly
+rounded, lo = the remainder rounded) for the descriptor's f64 atan2
+(sift-project_amd/csrc/sift_math64.h kAtanTab). Evaluated with 60-digit
+decimal arithmetic (argument halving + Taylor series)."""
 from decimal import Decimal, getcontext
 
 getcontext().prec = 60
@@ -24,4 +24,7 @@ def atan(x: Decimal) -> Decimal:
 
 
 if __name__ == "__main__":
-    print(", ".join(float(atan(Decimal(k) / 16)).hex() for k in range(17)))
+    for k in range(17):
+        v = atan(Decimal(k) / 16)
+        hi = float(v)
+        print(f"{{{hi.hex()}, {float(v - Decimal(hi)).hex()}}},")

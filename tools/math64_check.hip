@@ -22,7 +22,7 @@
 using namespace sift_amd;
 
 __global__ void k_eval(const double* a, const double* b, int n, double* mine, double* dev, int fn) {
-    __shared__ double tab[17];
+    __shared__ double2 tab[17];
     if (threadIdx.x < 17) tab[threadIdx.x] = kAtanTab[threadIdx.x];
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
