@@ -5,12 +5,21 @@ kernels' HBM GB/s against the chip's peak.
 
 A "step" is one full pass of detect_keypoints_and_descriptors (reference
 src/sift.cpp:712-776: pyramid, extrema, refine, orientation, clean,
-descriptors; the keypoints.png side effect excluded) over
---batch synthetic 1920x1080 images per GPU (BASELINE config 2 at N=1), with
-the input already resident in HBM and the final sorted keypoint records
-returned to the host. With N>1 ranks (torchrun) every rank processes its own
-images (weak scaling, BASELINE config 4) and the per-image descriptor
-buffers are all-gathered over RCCL each step.
+descriptors, every stage in f64 as the reference; the keypoints.png side
+effect excluded) over --batch synthetic 1920x1080 images
+per GPU (BASELINE config 2 at N=1), with the input already resident in HBM
+and the final sorted keypoint records returned to the host. With N>1 ranks
+(torchrun) every rank processes its own images (weak scaling, BASELINE
+config 4) and the per-image descriptor buffers are all-gathered over RCCL.
+
+roofline: the pyramid's algorithmic bytes of every image of the
+timed region / its wall time ("chip level"), with the kernel-alone figure
+(serialised context, dispatch-timestamped HIP events, comparable with the
+rocprofv3 summaries under profiles/) and the FP64-issue fraction beside it.
+After the timed region (N=1): kernel-alone legs, latency, API path, 8-image
+jobs, BASELINE configs 3 (4096^2) and 5 (8K) with their own rooflines, the
+CPU baselines (the oracle port and the reference itself, one core), the
+matcher and the stitching consumer.
 
 usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 """
@@ -35,11 +44,14 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, PROF_EXTREMA, PROF_PYRAMID,  # noqa: E402
-                      Context, SiftParams, synth_image)
+from sift_hip import (INPUT_F64_DEVICE, INPUT_F64_HOST, PROF_DESC, PROF_EXTREMA,  # noqa: E402
+                      PROF_ORIENT, PROF_PYRAMID, PROF_REFINE, Context, SiftParams, synth_image)
 
 METRIC = ("keypoints/sec (detect+describe) on 1920×1080; Gaussian-pyramid HBM GB/s vs peak")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# FP64 vector issue peak: 256 CUs x 4 SIMDs x 16 lanes per cycle x 2.4 GHz
+# (= 78.6 TFLOP/s counting an FMA as two), in lane-operations per second
+FP64_PEAK_OPS = 256 * 4 * 16 * 2.4e9
 
 
 def cpu_model() -> str:
@@ -77,6 +89,43 @@ def cpu_baseline(img: np.ndarray, seconds: float) -> dict:
                   f"reference's own copy-fixed code on the same core, whose column-major blur "
                   f"walk dominates it; single thread, {cpu_model()}), {t_total:.1f} s",
     }
+
+
+def cpu_baseline_reference(img: np.ndarray, seconds_hint: float) -> dict | None:
+    """The reference itself on the bench host: oracle/_ref/ref_harness_cf
+    (the reference's src/sift.cpp compiled by oracle/Makefile with its own
+    flags, copy-fixed — the four per-item deep copies made const refs,
+    outputs byte-identical to the as-is build) runs
+    detect_keypoints_and_descriptors' stages (sift.cpp:712-776, minus the
+    keypoints.png side effect) once on the same seed-42 image, single
+    threaded; its own steady-clock total is the time. None when the harness
+    was not built (it needs /root/reference at build time)."""
+    import subprocess
+    import tempfile
+
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness_cf")
+    if not os.path.exists(exe):
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        raw = os.path.join(d, "in.raw")
+        h, w = img.shape[:2]
+        c = 1 if img.ndim == 2 else img.shape[2]
+        with open(raw, "wb") as f:
+            f.write(b"SIFTRAW1" + np.array([w, h, c], dtype="<i4").tobytes())
+            f.write(np.ascontiguousarray(img, dtype="<f8").tobytes())
+        r = subprocess.run([exe, raw, os.path.join(d, "out")], capture_output=True, text=True,
+                           timeout=max(120.0, 20 * seconds_hint))
+        if r.returncode != 0:
+            return {"error": f"ref_harness_cf exit {r.returncode}: {r.stderr[-200:]}"}
+        meta = dict(line.split(None, 1) for line in open(os.path.join(d, "out.meta.txt")))
+    t, n = float(meta["time_total"]), int(meta["final"])
+    return {"value": n / t, "unit": "keypoints/s", "cores": 1, "kind": "reference",
+            "seconds": t, "keypoints": n,
+            "sample": f"1 x full 1920x1080 synthetic image (seed 42) through the reference's own "
+                      f"src/sift.cpp (oracle/_ref/ref_harness_cf: compiled from /root/reference "
+                      f"with its Makefile flags -std=c++17 -O3, copy-fixed const refs at "
+                      f"sift.cpp:311,346,466,616, byte-identical outputs); single thread, "
+                      f"{cpu_model()}; time = the harness's steady-clock total of the stages"}
 
 
 def matcher_bench(ctx, dev, kps_a, W, H, params, cpu_seconds: float) -> dict:
@@ -147,21 +196,157 @@ def roofline_obj(ms: float, nbytes: float, launches: int, traffic, note) -> dict
     }
 
 
+def chip_roofline(bytes_img: float, launches_img: float, images: int, elapsed: float, traffic,
+                  note) -> dict:
+    """Chip-level roofline of a kernel family over the timed region: its
+    algorithmic bytes for every image processed / the region's wall time.
+    `traffic` (PMC, per launch) is scaled to bytes per image."""
+    achieved = bytes_img * images / elapsed / 1e9
+    t_img = traffic["hbm_bytes_per_launch"] * launches_img if traffic else None
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": t_img,
+            "traffic_source": note, "traffic_unit": "HBM bytes per image",
+            "algorithmic_bytes_per_image": bytes_img,
+            "traffic_over_algorithmic": (t_img / bytes_img) if t_img else None,
+            "launches_per_image": launches_img,
+            "scope": "chip level: algorithmic bytes of every image of the timed region / its "
+                     "wall time (the kernels share the chip with every other stage)"}
+
+
+# BASELINE configs 3 and 5 (SURVEY 8d inputs; generator arguments as the
+# reference-generated goldens tests/golden/synth_4096x4096_int2_oct5.npz and
+# synth_7680x4320_dense.npz, which pin the HIP path's output on them)
+BIG_CONFIGS = {
+    "config3": {"w": 4096, "h": 4096, "nblobs": 300000, "smax": 6.0, "images": 8,
+                "params": {"intervals": 2, "max_octaves": 5},
+                "workload": "BASELINE config 3: single 4096x4096 synthetic image (seed 42, 300k "
+                            "blobs), 5 octaves x 5 scales (intervals=2, max_octaves=5)",
+                "reference_cpu": {"seconds": 109.7, "keypoints": 46242,
+                                  "source": "BASELINE.md (survey container, copy-fixed reference, "
+                                            "1 thread)"}},
+    "config5": {"w": 7680, "h": 4320, "nblobs": 1500000, "smax": 4.0, "images": 5,
+                "params": {},
+                "workload": "BASELINE config 5: 8K (7680x4320) dense synthetic image (seed 42, "
+                            "1.5M blobs), reference default parameters",
+                "reference_cpu": {"seconds": 206.5, "keypoints": 166313,
+                                  "source": "BASELINE.md (survey container, copy-fixed reference, "
+                                            "1 thread)"}},
+}
+
+
+def big_config_leg(name: str, dev) -> dict:
+    """One large image per job, JOB pairs in flight (two jobs: the next
+    image's pyramid overlaps the previous one's keypoint tail), input
+    resident in HBM: keypoints/s and ms per image; the pyramid's chip-level
+    HBM fraction over that time, its kernel-alone fraction and FP64-issue
+    fraction (SIFT_SERIAL context, dispatch-timestamped events), and the
+    keypoint kernels alone."""
+    spec = BIG_CONFIGS[name]
+    w, h = spec["w"], spec["h"]
+    p = SiftParams(**spec["params"])
+    img = synth_image(w, h, 1, nblobs=spec["nblobs"], smax=spec["smax"], seed=42)
+    t = torch.from_numpy(img).to(dev)
+    torch.cuda.synchronize()
+    ptr = [t.data_ptr()]
+    c = Context(dev.index)
+    sub = lambda k: c.submit(ptr, INPUT_F64_DEVICE, w, h, 1, p)  # noqa: E731
+    pipelined(c, sub, 2, 2)
+    n = spec["images"]
+    kp, dt = pipelined(c, sub, n, 2)
+    cnt = c.counts()
+    c.close()
+    dims = [(cnt["octave0_w"] >> o, cnt["octave0_h"] >> o) for o in range(cnt["octaves"])]
+    os.environ["SIFT_SERIAL"] = "1"
+    try:
+        sc = Context(dev.index)
+    finally:
+        del os.environ["SIFT_SERIAL"]
+    sc.detect_device(ptr[0], w, h, 1, p)
+    sc.profile_table(reset=True)
+    sc.set_profiling(True)
+    n_alone = 3
+    for _ in range(n_alone):
+        sc.detect_device(ptr[0], w, h, 1, p)
+    sc.set_profiling(False)
+    pyr, ext, kpk = _rows_roofline(sc.profile_table(reset=True), n_alone)
+    sc.close()
+    del t
+    torch.cuda.empty_cache()
+    pyr_b, ext_b = pyr["bytes_per_image"], ext["bytes_per_image"]
+    fp64 = pyramid_fp64_ops(dims, p)
+    ref = dict(spec["reference_cpu"])
+    ref["value"] = ref["keypoints"] / ref["seconds"]
+    roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "achieved": round(pyr_b * n / dt / 1e9, 1),
+            "frac": round(pyr_b * n / dt / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_image": pyr_b,
+            "scope": "chip level: pyramid bytes per image x images / wall time",
+            "alone": pyr,
+            "fp64": {"ops_per_image": fp64, "peak_ops_per_s": FP64_PEAK_OPS,
+                     "frac": fp64 * n / dt / FP64_PEAK_OPS,
+                     "frac_alone": fp64 / (pyr["us_per_image"] * 1e-6) / FP64_PEAK_OPS}}
+    return {"workload": spec["workload"], "image": f"{w}x{h}x1", "images": n, "jobs_in_flight": 2,
+            "value": kp / dt, "unit": "keypoints/s", "ms_per_image": dt / n * 1e3,
+            "keypoints_per_image": kp // n, "octaves": cnt["octaves"],
+            "levels_per_octave": cnt["levels_per_octave"], "dtype": "f64",
+            "roofline": roof,
+            "extrema_roofline": {"achieved": round(ext_b * n / dt / 1e9, 1),
+                                 "frac": round(ext_b * n / dt / 1e9 / HBM_PEAK_GBS, 4),
+                                 "alone": ext},
+            "keypoint_kernels_alone": kpk,
+            "reference_cpu": ref, "speedup_vs_reference_cpu": (kp / dt) / ref["value"]}
+
+
+def level_radii(params) -> list:
+    """Half-kernel radius R = ceil(3 sigma) (image.cpp:226) of the initial
+    blur (sigma = sqrt(s0^2 - 1), sift.cpp:124) and of levels 1..G-1
+    (sift.cpp:143-155)."""
+    import math
+    s0, iv = params.init_sigma, params.intervals
+    k = 2.0 ** (1.0 / iv)
+    sig = [math.sqrt(s0 * s0 - 1)] + [(k ** (i - 1)) * s0 * math.sqrt(k * k - 1)
+                                      for i in range(1, iv + 3)]
+    return [int(math.ceil(3 * x)) for x in sig]
+
+
+def pyramid_fp64_ops(octave_dims, params) -> float:
+    """FP64 lane-operations of one image's pyramid (algorithmic, no halo
+    redundancy): per output pixel and pass the reference's
+    acc = v*k0; acc += k[u]*(v[+u] + v[-u]) (3R+1 ops) and the correctly
+    rounded division by sum_w (3: mul, fma, fma), two passes per level
+    (image.cpp:168-211)."""
+    R = level_radii(params)
+    n0 = octave_dims[0][0] * octave_dims[0][1]
+    ops = 2 * (3 * R[0] + 4) * n0
+    for (w, h) in octave_dims:
+        ops += sum(2 * (3 * r + 4) * w * h for r in R[1:])
+    return float(ops)
+
+
 def _rows_roofline(prof, n_images):
+    """Kernel-alone figures from dispatch-timestamped events (SIFT_SERIAL
+    context: every kernel alone on the chip)."""
     rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
     ms, nb, n = (sum(r[k] for r in rows) for k in range(3))
     pyr = roofline_obj(ms, nb, n, None, None)
     pyr["us_per_image"] = ms * 1e3 / n_images
+    pyr["bytes_per_image"] = nb / n_images
     pyr["per_octave"] = [{"octave": o, "us_per_launch": m * 1e3 / k,
+                          "us_per_image": m * 1e3 / n_images,
                           "achieved_GBps": b / (m * 1e-3) / 1e9}
                          for o, (m, b, k) in enumerate(rows) if k]
     ems, eb, en = prof[PROF_EXTREMA]
     ext = roofline_obj(ems, eb, en, None, None)
     ext["us_per_image"] = ems * 1e3 / n_images
+    ext["bytes_per_image"] = eb / n_images
     for d in (pyr, ext):
         for k in ("traffic", "traffic_source", "traffic_over_algorithmic"):
             d.pop(k)
-    return pyr, ext
+    kp = {name: {"us_per_image": prof[row][0] * 1e3 / n_images,
+                 "launches_per_image": prof[row][2] / n_images}
+          for name, row in (("refine", PROF_REFINE), ("orientation", PROF_ORIENT),
+                            ("descriptor", PROF_DESC))}
+    return pyr, ext, kp
 
 
 def alone_leg(dev_img, W, H, params, n_images: int = 200, batch_imgs=None) -> dict:
@@ -184,10 +369,11 @@ def alone_leg(dev_img, W, H, params, n_images: int = 200, batch_imgs=None) -> di
         sctx.detect_device(dev_img.data_ptr(), W, H, 1, params)
     dt = time.perf_counter() - t0
     sctx.set_profiling(False)
-    pyr, ext = _rows_roofline(sctx.profile_table(reset=True), n_images)
+    pyr, ext, kp = _rows_roofline(sctx.profile_table(reset=True), n_images)
     note = (f"SIFT_SERIAL=1 context, {n_images} synchronous detects of the same image, every "
-            f"kernel alone on the chip; {dt / n_images * 1e3:.3f} ms per image serialised")
-    out = {"pyramid": pyr, "extrema": ext, "note": note}
+            f"kernel alone on the chip, per-launch dispatch-timestamped HIP events; "
+            f"{dt / n_images * 1e3:.3f} ms per image serialised")
+    out = {"pyramid": pyr, "extrema": ext, "keypoint_kernels": kp, "note": note}
     if batch_imgs:
         # BASELINE config 4's per-GPU share: one 8-image job per launch, alone
         ptrs = [t.data_ptr() for t in batch_imgs]
@@ -199,8 +385,8 @@ def alone_leg(dev_img, W, H, params, n_images: int = 200, batch_imgs=None) -> di
         for _ in range(nb_jobs):
             sctx.fetch(sctx.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params))
         sctx.set_profiling(False)
-        bp, be = _rows_roofline(sctx.profile_table(reset=True), nb_jobs * len(ptrs))
-        out["batch"] = {"pyramid": bp, "extrema": be,
+        bp, be, bk = _rows_roofline(sctx.profile_table(reset=True), nb_jobs * len(ptrs))
+        out["batch"] = {"pyramid": bp, "extrema": be, "keypoint_kernels": bk,
                         "note": f"{nb_jobs} jobs of {len(ptrs)} 1920x1080 images (one launch per "
                                 f"kernel covers the job), SIFT_SERIAL=1 context"}
     sctx.close()
@@ -208,15 +394,15 @@ def alone_leg(dev_img, W, H, params, n_images: int = 200, batch_imgs=None) -> di
 
 
 def desc_modes_leg(ptrs, W, H, params, n_steps: int, depth: int, rounds: int = 4) -> dict:
-    """The timed region's pipelined step on two fresh contexts whose
-    descriptor kernel runs in SIFT_DESC_MODE 1 (the default: exact f64
-    sample acceptance, f32 sample math, f64 histograms) and 0 (every
-    per-sample operation in f64, as src/sift.cpp:641-678), in interleaved
-    blocks (the boxes drift by several % run to run; the ratio holds)."""
+    """The timed region's pipelined step on fresh contexts whose descriptor
+    kernel runs in SIFT_DESC_MODE 0 (the default: k_descriptor_split, every
+    per-sample operation in f64 as src/sift.cpp:641-678) and 1 (round 3's
+    k_descriptor_wave, f32 sample math), in interleaved blocks (the boxes
+    drift by several % run to run; the ratio holds)."""
     prev = os.environ.get("SIFT_DESC_MODE")
     ctxs = {}
     try:
-        for mode in (1, 0):
+        for mode in (0, 1):
             os.environ["SIFT_DESC_MODE"] = str(mode)
             ctxs[mode] = Context(torch.cuda.current_device())
     finally:
@@ -231,7 +417,7 @@ def desc_modes_leg(ptrs, W, H, params, n_steps: int, depth: int, rounds: int = 4
         pipelined(c, lambda k, c=c: c.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params),
                   4 * depth, depth)
     for r in range(rounds):
-        for m in ((1, 0) if r % 2 == 0 else (0, 1)):
+        for m in ((0, 1) if r % 2 == 0 else (1, 0)):
             c = ctxs[m]
             k, t = pipelined(c, lambda k, c=c: c.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params),
                              block, depth)
@@ -242,7 +428,7 @@ def desc_modes_leg(ptrs, W, H, params, n_steps: int, depth: int, rounds: int = 4
     return {f"desc_mode_{m}": {"value": kp[m] / dt[m], "unit": "keypoints/s",
                                "ms_per_step": dt[m] / (block * rounds) * 1e3,
                                "steps": block * rounds}
-            for m in (1, 0)}
+            for m in (0, 1)}
 
 
 def host_busy_leg(ctx, ptrs, W, H, params, n_steps: int, depth: int) -> dict:
@@ -414,16 +600,19 @@ def main() -> int:
     ap.add_argument("--sync", action="store_true",
                     help="one job at a time (no pipelining), for profiling / A-B")
     ap.add_argument("--no-desc-f64", action="store_true",
-                    help="skip the all-f64 descriptor leg (value_desc_f64)")
+                    help="(kept for old command lines: the default descriptor is all-f64)")
+    ap.add_argument("--desc-ab", action="store_true",
+                    help="steady-state A/B of the descriptor variants (desc_modes_leg)")
+    ap.add_argument("--no-big", action="store_true",
+                    help="skip the BASELINE config 3 / config 5 legs (4096^2, 8K)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the latency / API / batch8 legs")
     ap.add_argument("--extra-seconds", type=float, default=2.0)
     ap.add_argument("--no-events", action="store_true",
-                    help="skip the per-launch HIP events of the pyramid roofline")
-    ap.add_argument("--events-every", type=int, default=8,
-                    help="time the pyramid/extrema launches of every k-th job of the timed "
-                         "region with HIP events (per-launch events on every job slow the "
-                         "pipeline by ~5%%)")
+                    help="no per-launch HIP events anywhere (the kernel-alone legs need them)")
+    ap.add_argument("--events-every", type=int, default=0,
+                    help="diagnostics: time the pyramid launches of every k-th job of the timed "
+                         "region with HIP events (0: none; events slow the pipeline)")
     ap.add_argument("--step-log", action="store_true",
                     help="print the timed region's submit / fetch / done times to stderr")
     ap.add_argument("--no-alone", action="store_true",
@@ -492,13 +681,14 @@ def main() -> int:
 
     depth = JOB_DEPTH if B == 1 else BATCH_DEPTH
 
-    sample_events = False  # set for the timed region
+    sample_events = False  # per-launch events on sampled jobs (--events-every)
+    in_timed = False  # set for the timed region
 
     step_log = []  # --step-log: (event, job, t) of the timed region
 
     def run(n_steps: int) -> int:
         kp = 0
-        log = step_log.append if (args.step_log and sample_events) else None
+        log = step_log.append if (args.step_log and in_timed) else None
         if args.sync:
             for k in range(n_steps):
                 if sample_events:
@@ -522,6 +712,19 @@ def main() -> int:
 
     run(max(1, args.warmup))
     kp_per_image = ctx.counts()["final_n"] // B
+    # the pyramid's / extrema scan's algorithmic bytes and launches per image,
+    # from the library's per-launch accounting on one profiled job
+    ctx.profile_table(reset=True)
+    ctx.set_profiling(True)
+    ctx.fetch(submit())
+    ctx.set_profiling(False)
+    prof0 = ctx.profile_table(reset=True)
+    pyr_bytes_img = sum(r[1] for r in prof0[PROF_PYRAMID:PROF_PYRAMID + 16]) / B
+    pyr_launches_img = sum(r[2] for r in prof0[PROF_PYRAMID:PROF_PYRAMID + 16]) / B
+    ext_bytes_img = prof0[PROF_EXTREMA][1] / B
+    ext_launches_img = prof0[PROF_EXTREMA][2] / B
+    cnt = ctx.counts()
+    dims = [(cnt["octave0_w"] >> o, cnt["octave0_h"] >> o) for o in range(cnt["octaves"])]
     if use_exchange:
         from sift_dist import RecordExchange, agree_capacity
         exchange = RecordExchange(agree_capacity(max_rows * args.exchange_steps, dev), dev,
@@ -534,6 +737,7 @@ def main() -> int:
     torch.cuda.synchronize()
     sample_events = not args.no_events and args.events_every > 0
     sample_events_used = sample_events
+    in_timed = True
     ctx.profile_table(reset=True)
     t0 = time.perf_counter()
     kp_total = run(args.steps)
@@ -547,13 +751,9 @@ def main() -> int:
         print("step log (ms from the timed region's start):", file=sys.stderr)
         for ev, k, t in step_log:
             print(f"  {ev:6s} job {k:3d} {1e3 * (t - t0):8.3f}", file=sys.stderr)
-    sample_events = False
+    sample_events = in_timed = False
     ctx.set_profiling(False)
     prof = ctx.profile_table(reset=True)
-    pyr_rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
-    blur_ms = sum(r[0] for r in pyr_rows)
-    blur_bytes = sum(r[1] for r in pyr_rows)
-    blur_launches = sum(r[2] for r in pyr_rows)
 
     exchange_check = None
     if use_exchange:
@@ -593,21 +793,26 @@ def main() -> int:
 
     if rank == 0:
         traffic, traffic_note = load_traffic(args.traffic_json)
-        roofline = roofline_obj(blur_ms, blur_bytes, blur_launches,
-                                traffic.get("pyramid") if traffic else None, traffic_note)
-        roofline["sampled_jobs"] = (f"per-launch HIP events on every {args.events_every}th job of "
-                                    "the timed region" if sample_events_used else None)
+        images = args.steps * B * world
+        # headline roofline, chip level: the algorithmic pyramid
+        # bytes of every image of the timed region over its wall time; the
+        # kernel-alone figure (serialised context, dispatch-timestamped
+        # events; rocprofv3 --kernel-trace of the same shape agrees,
+        # profiles/) sits beside it
+        roofline = chip_roofline(pyr_bytes_img, pyr_launches_img, images, elapsed,
+                                 traffic.get("pyramid") if traffic else None, traffic_note)
         roofline["kernel"] = ("Gaussian pyramid: k_blur (strip walk, octave 0 incl. the fused "
                               "gray/x2 initial blur) + k_blur_tile (LDS tiles, octaves >= 1) + "
                               "k_octaves_lds (LDS-resident small octaves); 16 B per pixel per "
-                              "level + 8 B per decimated pixel")
-        roofline["per_octave"] = [
-            {"octave": o, "launches": n, "us_per_launch": ms * 1e3 / n,
-             "achieved_GBps": b / (ms * 1e-3) / 1e9}
-            for o, (ms, b, n) in enumerate(pyr_rows) if n]
-        ems, eb, en = prof[PROF_EXTREMA]
-        extrema_roofline = roofline_obj(ems, eb, en, traffic.get("extrema") if traffic else None,
-                                        traffic_note)
+                              "level + 8 B per decimated pixel (SURVEY 8d)")
+        fp64_img = pyramid_fp64_ops(dims, params)
+        roofline["fp64"] = {"ops_per_image": fp64_img, "peak_ops_per_s": FP64_PEAK_OPS,
+                            "frac": fp64_img * images / elapsed / FP64_PEAK_OPS,
+                            "note": "FP64 lane-operations of the pyramid, 2(3R+4) per pixel per "
+                                    "level (two passes; FMA = 1), over the same wall time"}
+        extrema_roofline = chip_roofline(ext_bytes_img, ext_launches_img, images, elapsed,
+                                         traffic.get("extrema") if traffic else None,
+                                         traffic_note)
         extrema_roofline["kernel"] = ("k_extrema_stream (DoG on the fly, 3x3x3 non-strict test): "
                                       "8 B x (intervals+3) levels per scanned pixel")
         out = {
@@ -622,11 +827,10 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "dtype_note": ("pyramid, DoG, extrema, refine, orientation and all histograms in f64 "
-                           "(the reference's arithmetic); the default descriptor (desc_mode 1) "
-                           "decides sample acceptance in f64 and does the per-sample math "
-                           "(rotation, magnitude, atan2, exp, trilinear weights) in f32; "
-                           "value_desc_f64 is the all-f64 descriptor (desc_mode 0)"),
+            "dtype_note": ("every stage in f64 as the reference: pyramid, DoG, extrema, refine, "
+                           "orientation and the descriptor's per-sample math (rotation, "
+                           "magnitude, atan2, exp, trilinear weights; desc_mode 0) with f64 "
+                           "histograms"),
             "data": "synthetic (deterministic integer-RNG generator: sinusoid + Gaussian blobs, "
                     "~w*h/52 blobs, sigma 1.5-7.5)",
             "config": {
@@ -636,7 +840,7 @@ def main() -> int:
                 "image": f"{W}x{H}x1",
                 "images_per_gpu_per_step": B,
                 "jobs_in_flight": depth,
-                "desc_mode": int(os.environ.get("SIFT_DESC_MODE", "1")),
+                "desc_mode": int(os.environ.get("SIFT_DESC_MODE", "0")),
                 "keypoints_per_image": kp_per_image,
                 "parallelism": f"image-sharded x{world}" + (
                     ", RCCL all-gather of the descriptor records straight from HBM "
@@ -647,38 +851,44 @@ def main() -> int:
             "extrema_roofline": extrema_roofline,
         }
         out["timed_region_s"] = elapsed
-        if world == 1 and not args.no_events and not args.no_alone:
+        if sample_events_used:
+            prof_rows = prof[PROF_PYRAMID:PROF_PYRAMID + 16]
+            out["timed_region_events"] = {
+                "every": args.events_every,
+                "pyramid_us_per_launch": [ms * 1e3 / n for ms, _, n in prof_rows if n],
+                "note": "per-launch events on sampled jobs while four jobs share the chip "
+                        "(launches overlap; not a kernel-quality figure)"}
+        if world == 1 and not args.no_alone and not args.no_events:
             b8 = [torch.from_numpy(synth_image(W, H, 1, seed=42 + i)).to(dev) for i in range(8)]
             alone = alone_leg(dev_imgs[0], W, H, params, batch_imgs=b8)
             del b8
             roofline["alone"] = alone["pyramid"]
             roofline["alone"]["note"] = alone["note"]
+            roofline["fp64"]["frac_alone"] = (fp64_img / (alone["pyramid"]["us_per_image"] * 1e-6)
+                                              / FP64_PEAK_OPS)
             extrema_roofline["alone"] = alone["extrema"]
             roofline["alone_batch8"] = alone["batch"]["pyramid"]
             roofline["alone_batch8"]["note"] = alone["batch"]["note"]
             extrema_roofline["alone_batch8"] = alone["batch"]["extrema"]
+            out["keypoint_kernels_alone"] = alone["keypoint_kernels"]
+            out["keypoint_kernels_alone_batch8"] = alone["batch"]["keypoint_kernels"]
         if world == 1 and not args.no_extra:
             out["host_busy"] = host_busy_leg(ctx, ptrs, W, H, params, max(args.steps, 400), depth)
-        if world == 1 and not args.no_desc_f64:
-            leg = desc_modes_leg(ptrs, W, H, params, max(args.steps, 800), depth)
-            out["value_desc_f64"] = leg["desc_mode_0"]["value"]
-            out["value_desc_f64_note"] = (
-                "steady state (desc_modes_leg: fresh contexts, interleaved blocks of pipelined "
-                "steps), not the 20-step shape of `value`; compare it with "
-                "desc_modes_leg.desc_mode_1, measured the same way: the all-f64 descriptor "
-                f"runs at {leg['desc_mode_0']['value'] / leg['desc_mode_1']['value']:.3f} of the "
-                "default's rate")
-            leg["note"] = ("pipelined steps as the timed region, on two fresh contexts in "
-                           "interleaved blocks: desc_mode 1 (default, f32 sample math) and "
-                           "desc_mode 0 (all-f64 descriptor, the reference's precision)")
-            out["desc_modes_leg"] = leg
+        if world == 1 and args.desc_ab:
+            out["desc_modes_leg"] = desc_modes_leg(ptrs, W, H, params, max(args.steps, 800), depth)
         if exchange_check is not None:
             out["exchange_check"] = exchange_check
         if world == 1 and not args.no_extra:
             out.update(extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params,
                                   args.extra_seconds))
+        if world == 1 and not args.no_big:
+            for name in ("config3", "config5"):
+                out[name] = big_config_leg(name, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(host_imgs[0], args.cpu_seconds)
+            ref = cpu_baseline_reference(host_imgs[0], args.cpu_seconds)
+            if ref is not None:
+                out["cpu_baseline_reference"] = ref
         if world == 1 and not args.no_matcher:
             kps_a, _ = ctx.detect_device(dev_imgs[0].data_ptr(), W, H, 1, params)
             out["matcher"] = matcher_bench(ctx, dev, kps_a, W, H, params,

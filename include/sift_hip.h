@@ -345,10 +345,15 @@ int sift_hip_blur_profile(sift_ctx* ctx, double* ms, int64_t* launches,
 /* The same per row: SIFT_PROF_PYRAMID + o = pyramid launches of octave o
  * (the LDS-resident small-octave launch counts under its first octave),
  * SIFT_PROF_EXTREMA = extrema launches (algorithmic bytes: every Gaussian
- * level read once per pixel). Each array holds SIFT_PROF_ROWS entries. */
+ * level read once per pixel), SIFT_PROF_REFINE / _ORIENT / _DESC = the
+ * keypoint stages' launches (bytes 0). Each array holds SIFT_PROF_ROWS
+ * entries. */
 #define SIFT_PROF_PYRAMID 0
 #define SIFT_PROF_EXTREMA 16
-#define SIFT_PROF_ROWS 17
+#define SIFT_PROF_REFINE 17
+#define SIFT_PROF_ORIENT 18
+#define SIFT_PROF_DESC 19
+#define SIFT_PROF_ROWS 20
 int sift_hip_profile_table(sift_ctx* ctx, double* ms, double* bytes, int64_t* launches,
                            int reset);
 

@@ -598,18 +598,23 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
             SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
                                             cand, lab, 0, nullptr, sx, nullptr, nullptr));
     }
+    hipEvent_t r0, r1, q0, q1, d0, d1;  // profiling events of the keypoint stages
+    if (prof_events(ctx, s, &r0, &r1, 0.0, SIFT_PROF_REFINE) != SIFT_OK ||
+        prof_events(ctx, s, &q0, &q1, 0.0, SIFT_PROF_ORIENT) != SIFT_OK ||
+        prof_events(ctx, s, &d0, &d1, 0.0, SIFT_PROF_DESC) != SIFT_OK)
+        return SIFT_ERR_HIP;
     SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
-                               raw, live + 1, cap_raw, sx));
+                               raw, live + 1, cap_raw, sx, r0, r1));
     if (lab && (ctx->lab_double & 4u))
         SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0,
                                    cap_cand, raw, lab + 1, 0, sx));
     SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
-                               cap_ori, work, ori_wgs, ori_mode, sx));
+                               cap_ori, work, ori_wgs, ori_mode, sx, q0, q1));
     if (lab && (ctx->lab_double & 8u))
         SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, lab + 2,
                                    0, lab + 3, ori_wgs, ori_mode, sx));
     SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
-                                   work + 2, c.ex, desc_wgs, desc_mode, sx));
+                                   work + 2, c.ex, desc_wgs, desc_mode, sx, d0, d1));
     if (lab && (ctx->lab_double & 16u))
         SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, nullptr,
                                        lab + 4, ExportSink{nullptr, nullptr, nullptr, 0},

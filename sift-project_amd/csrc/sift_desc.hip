@@ -663,19 +663,17 @@ hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* 
                              const RecSide* rec_side, const unsigned* rec_begin,
                              const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
                              unsigned* work, const ExportSink& ex, unsigned wgs,
-                             int mode, hipStream_t s) {
+                             int mode, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     // persistent: workgroups pull records
     if (mode == 1) {  // four waves per workgroup, a record per wave (f32 sample math)
         const unsigned blocks = std::min<unsigned>(wgs, cap_rec > 0 ? (cap_rec + 3) / 4 : 1);
-        hipLaunchKernelGGL(k_descriptor_wave, dim3(blocks), dim3(256), 0, s, d_pt, P, recs,
-                           rec_side, rec_begin, n_rec, cap_rec, desc_f32, work, ex);
-        return hipGetLastError();
+        return launch_timed(k_descriptor_wave, dim3(blocks), dim3(256), 0, s, e0, e1, d_pt, P,
+                            recs, rec_side, rec_begin, n_rec, cap_rec, desc_f32, work, ex);
     }
     const unsigned blocks = std::min<unsigned>(wgs, cap_rec > 0 ? cap_rec : 1);
     auto kern = mode == 2 ? k_descriptor_split<false> : k_descriptor_split<true>;
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, d_pt, P, recs, rec_side, rec_begin,
-                       n_rec, cap_rec, desc_f32, work, ex);
-    return hipGetLastError();
+    return launch_timed(kern, dim3(blocks), dim3(256), 0, s, e0, e1, d_pt, P, recs, rec_side,
+                        rec_begin, n_rec, cap_rec, desc_f32, work, ex);
 }
 
 }  // namespace sift_amd

@@ -3,6 +3,7 @@
 // descriptors). Internal to the library.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "sift_types.h"
@@ -79,6 +80,18 @@ __device__ __forceinline__ double div_sum_w(double a, double s, double inv) {
     const double q = a * inv;
     const double r = __builtin_fma(-q, s, a);
     return __builtin_fma(r, inv, q);
+}
+
+// Launch with optional HIP events whose start/stop timestamps ride on the
+// dispatch packet itself (no extra barrier packets between kernels).
+template <class K, class... Args>
+static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                               hipEvent_t e0, hipEvent_t e1, Args... args) {
+    if (e0 && e1)
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, e0, e1, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+    return hipGetLastError();
 }
 
 }  // namespace

@@ -63,7 +63,8 @@ hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, i
                            int w1 = 4);
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
-                         RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s);
+                         RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s,
+                         hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // orientation of raw keypoints [*raw_begin, *n_raw) -> records appended at
 // n_rec; descriptors of records [*rec_begin, *n_rec). `work`: two zeroed
 // device words per launch (work counter, done counter); ex.cnt receives the
@@ -71,12 +72,14 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
-                         unsigned* work, unsigned wgs, int mode, hipStream_t s);
+                         unsigned* work, unsigned wgs, int mode, hipStream_t s,
+                         hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
                              const RecSide* rec_side, const unsigned* rec_begin,
                              const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
                              unsigned* work, const ExportSink& ex, unsigned wgs,
-                             int mode, hipStream_t s);
+                             int mode, hipStream_t s, hipEvent_t e0 = nullptr,
+                             hipEvent_t e1 = nullptr);
 
 // out[i] = recs[items[i].src] with size = items[i].size (final records on the device)
 hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, unsigned n,

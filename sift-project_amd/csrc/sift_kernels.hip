@@ -1706,17 +1706,6 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
 // ---------------------------------------------------------------------------
 // launch helpers
 // ---------------------------------------------------------------------------
-template <class K, class... Args>
-static hipError_t launch_timed(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s,
-                               hipEvent_t e0, hipEvent_t e1, Args... args) {
-    // With events, the start/stop timestamps ride on the dispatch packet
-    // itself (no extra barrier packets between kernels).
-    if (e0 && e1)
-        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, e0, e1, 0, args...);
-    else
-        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
-    return hipGetLastError();
-}
 
 template <int R, int C, int MODE>
 static hipError_t launch_blur_r(const BlurSource& src, double* dst, size_t bs, int n_img, int W,
@@ -2103,7 +2092,8 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_i
 
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
-                         RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s) {
+                         RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s,
+                         hipEvent_t e0, hipEvent_t e1) {
     // SIFT_REFINE_NT (64 or 256 threads per workgroup), SIFT_REFINE_WGS: A/B knobs
     static const int nt = [] {
         const char* e = std::getenv("SIFT_REFINE_NT");
@@ -2122,38 +2112,32 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
     unsigned blocks = (cap_cand + per_wg - 1) / per_wg;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks == 0) blocks = 1;
-#define SIFT_REFINE_LAUNCH(NT_, CPW_)                                                          \
-    hipLaunchKernelGGL((k_refine<NT_, CPW_>), dim3(blocks), dim3(NT_), 0, s, d_pt, P, cand,   \
-                       cand_begin, n_cand, cap_cand, out, n_out, cap_out)
-    if (nt == 256)
-        SIFT_REFINE_LAUNCH(256, 64);
-    else if (cpw == 16)
-        SIFT_REFINE_LAUNCH(64, 16);
-    else if (cpw == 32)
-        SIFT_REFINE_LAUNCH(64, 32);
-    else
-        SIFT_REFINE_LAUNCH(64, 64);
+#define SIFT_REFINE_LAUNCH(NT_, CPW_)                                                           \
+    launch_timed(k_refine<NT_, CPW_>, dim3(blocks), dim3(NT_), 0, s, e0, e1, d_pt, P, cand,    \
+                 cand_begin, n_cand, cap_cand, out, n_out, cap_out)
+    if (nt == 256) return SIFT_REFINE_LAUNCH(256, 64);
+    if (cpw == 16) return SIFT_REFINE_LAUNCH(64, 16);
+    if (cpw == 32) return SIFT_REFINE_LAUNCH(64, 32);
+    return SIFT_REFINE_LAUNCH(64, 64);
 #undef SIFT_REFINE_LAUNCH
-    return hipGetLastError();
 }
 
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
-                         unsigned* work, unsigned wgs, int mode, hipStream_t s) {
+                         unsigned* work, unsigned wgs, int mode, hipStream_t s,
+                         hipEvent_t e0, hipEvent_t e1) {
     unsigned blocks = wgs;  // persistent: workgroups pull keypoints
     if (mode == 1) {  // four waves per workgroup, a keypoint per wave
         blocks = std::min<unsigned>(blocks, cap_raw > 0 ? (cap_raw + 3) / 4 : 1);
         const size_t lds = (size_t)4 * ori_wave_lds_doubles(P.num_bins) * sizeof(double);
-        hipLaunchKernelGGL(k_orient_wave, dim3(blocks), dim3(256), lds, s, d_pt, P, raw,
-                           raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work);
-        return hipGetLastError();
+        return launch_timed(k_orient_wave, dim3(blocks), dim3(256), lds, s, e0, e1, d_pt, P, raw,
+                            raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work);
     }
     if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
     const size_t lds = (size_t)(4 * kOriReps * (P.num_bins + 2) + kOriTab) * sizeof(double);
-    hipLaunchKernelGGL(k_orient, dim3(blocks), dim3(256), lds, s, d_pt, P, raw, raw_begin, n_raw,
-                       cap_raw, recs, rec_side, n_rec, cap_rec, work);
-    return hipGetLastError();
+    return launch_timed(k_orient, dim3(blocks), dim3(256), lds, s, e0, e1, d_pt, P, raw,
+                        raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work);
 }
 
 }  // namespace sift_amd

@@ -44,7 +44,7 @@ MATCH_DTYPE = np.dtype([("i1", "<u4"), ("i2", "<u4"), ("distance", "<f8")])
 INPUT_F64_HOST, INPUT_F64_DEVICE, INPUT_U8_HOST, INPUT_U8_DEVICE = 0, 1, 2, 3
 MAX_BATCH = 16
 MAX_INFLIGHT = 8
-PROF_PYRAMID, PROF_EXTREMA, PROF_ROWS = 0, 16, 17
+PROF_PYRAMID, PROF_EXTREMA, PROF_REFINE, PROF_ORIENT, PROF_DESC, PROF_ROWS = 0, 16, 17, 18, 19, 20
 
 ERRORS = {
     0: "ok",

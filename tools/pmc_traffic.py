@@ -21,7 +21,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KNOWN = 96 * 2 ** 20 * 8  # bytes moved each way per calibration launch
 KERNEL_SOURCES = ("sift-project_amd/csrc/sift_kernels.hip", "sift-project_amd/csrc/sift_kernels.h",
-                  "sift-project_amd/csrc/sift_types.h")
+                  "sift-project_amd/csrc/sift_device.h", "sift-project_amd/csrc/sift_types.h")
 
 
 def kernel_src_sha256(root=ROOT):
@@ -73,7 +73,8 @@ def main(d, out):
         res[f] = {"hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd,
                   "write_bytes_per_launch": wr, "launches": n[f]}
     if bench is not None:
-        alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+        r = bench["roofline"]
+        alg = r["algorithmic_bytes_per_image"] / r["launches_per_image"]
         res["pyramid"]["algorithmic_bytes_per_launch"] = alg
         res["pyramid"]["traffic_over_algorithmic"] = res["pyramid"]["hbm_bytes_per_launch"] / alg
     json.dump(res, open(out, "w"), indent=1)
