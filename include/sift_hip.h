@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SIFT_HIP_ABI_VERSION 2
+#define SIFT_HIP_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define SIFT_OK 0
@@ -38,6 +38,7 @@ extern "C" {
 #define SIFT_ERR_NO_DEVICE -6    /* no HIP device / bad device index           */
 #define SIFT_ERR_PARAM -7        /* parameter outside the supported range      */
 #define SIFT_ERR_STATE -8        /* call order violated (e.g. no prior detect) */
+#define SIFT_ERR_NO_COMM -9      /* RCCL missing or a collective failed        */
 
 /*
  * Parameters of detect_keypoints_and_descriptors (reference sift.hh:65-71),
@@ -199,6 +200,49 @@ int sift_hip_fetch_device_async(sift_ctx* ctx, int ticket, void* d_out, size_t c
 int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_t slot_bytes,
                           int hdr_rows, int count_word, int sum_word, int n_sum_words,
                           size_t cap_rows, uint64_t* d_bad, void* stream);
+
+/* ---- multi-GPU record exchange without torch ----- */
+/*
+ * A batch of images shards one image per GPU (rank r detects images
+ * i % nranks == r; the reference function is pure per image,
+ * src/sift.cpp:712-776). These give a C++ batch driver the one exchange:
+ * every rank receives every image's final records, over RCCL (xGMI) in two
+ * phases, since RCCL has no all-gather-v: the ranks' (image id, count)
+ * tables, then the records padded to the largest rank's count (padding
+ * dropped on the device). Same bytes as the torch path
+ * (sift-project_amd/sift_dist.py allgather_records). RCCL is loaded on first
+ * use (dlopen librccl.so.1); SIFT_ERR_NO_COMM when it is missing.
+ *
+ * Communicators: sift_hip_comm_init_all — one process drives every listed
+ * device (ncclCommInitAll; comms[i] is rank i on devices[i]); then call
+ * sift_hip_allgather_records for every rank concurrently, one host thread
+ * per rank. Or one process per GPU: rank 0 gets an id with
+ * sift_hip_comm_unique_id, shares it out of band, every rank calls
+ * sift_hip_comm_init_rank.
+ */
+#define SIFT_COMM_ID_BYTES 128
+typedef struct sift_comm sift_comm;
+int sift_hip_comm_unique_id(unsigned char id[SIFT_COMM_ID_BYTES]);
+int sift_hip_comm_init_rank(const unsigned char id[SIFT_COMM_ID_BYTES], int nranks, int rank,
+                            int device, sift_comm** out);
+int sift_hip_comm_init_all(int n_devices, const int* devices, sift_comm** comms);
+int sift_hip_comm_destroy(sift_comm* comm);
+int sift_hip_comm_rank(const sift_comm* comm, int* rank, int* nranks);
+
+/* Collective over every rank of `comm` (each rank calls it once, with the
+ * same max_local). This rank's n_local (<= max_local) images: image ids[j]
+ * has counts[j] final records, image-major in d_recs (device memory, e.g.
+ * from sift_hip_fetch_device). On return every rank's d_out (device, cap_out
+ * records) holds all ranks' records rank-major (rank 0's images in its
+ * order, then rank 1's, ...), *n_out their total, and the host arrays
+ * out_ids / out_counts (nranks * max_local entries, rank-major, id -1 for an
+ * empty entry) describe them. Blocking (the host waits for the counts and
+ * the final copies); `stream` optional. *n_out > cap_out: SIFT_ERR_ARG after
+ * the collectives completed, nothing written to d_out. */
+int sift_hip_allgather_records(sift_comm* comm, const sift_kp* d_recs, const int64_t* ids,
+                               const size_t* counts, int n_local, int max_local, sift_kp* d_out,
+                               size_t cap_out, int64_t* out_ids, size_t* out_counts,
+                               size_t* n_out, void* stream);
 
 /* submit + wait + fetch into library-allocated storage (sift_hip_free):
  * *out_kps image-major, counts[b] per image. */

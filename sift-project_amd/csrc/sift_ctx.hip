@@ -1885,6 +1885,7 @@ const char* sift_hip_strerror(int status) {
         case SIFT_ERR_NO_DEVICE: return "no such HIP device";
         case SIFT_ERR_PARAM: return "parameter outside the supported range";
         case SIFT_ERR_STATE: return "invalid call order (no such job / no previous detect / too many jobs in flight)";
+        case SIFT_ERR_NO_COMM: return "RCCL unavailable or a collective failed";
         default: return "unknown error";
     }
 }

@@ -56,6 +56,7 @@ ERRORS = {
     -6: "no such HIP device",
     -7: "parameter outside the supported range",
     -8: "invalid call order (no such job / no previous detect / too many jobs in flight)",
+    -9: "RCCL unavailable or a collective failed",
 }
 
 # exported symbols declared in include/sift_hip.h
@@ -73,6 +74,12 @@ EXPORTS = (
     "sift_hip_fetch_device",
     "sift_hip_fetch_device_async",
     "sift_hip_verify_slots",
+    "sift_hip_comm_unique_id",
+    "sift_hip_comm_init_rank",
+    "sift_hip_comm_init_all",
+    "sift_hip_comm_destroy",
+    "sift_hip_comm_rank",
+    "sift_hip_allgather_records",
     "sift_hip_detect_batch",
     "sift_hip_match",
     "sift_hip_match_device",
@@ -193,6 +200,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     if hasattr(lib, "sift_hip_fetch_device_async"):  # (absent from older A/B builds)
         lib.sift_hip_fetch_device_async.argtypes = [vp, i, vp, sz, vp, vp]
         lib.sift_hip_verify_slots.argtypes = [vp, vp, i, sz, i, i, i, i, sz, vp, vp]
+    if hasattr(lib, "sift_hip_comm_init_all"):  # (absent from older A/B builds)
+        lib.sift_hip_comm_unique_id.argtypes = [vp]
+        lib.sift_hip_comm_init_rank.argtypes = [vp, i, i, i, ctypes.POINTER(vp)]
+        lib.sift_hip_comm_init_all.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp)]
+        lib.sift_hip_comm_destroy.argtypes = [vp]
+        lib.sift_hip_comm_rank.argtypes = [vp, ctypes.POINTER(i), ctypes.POINTER(i)]
+        lib.sift_hip_allgather_records.argtypes = [vp, vp, vp, vp, i, i, vp, sz, vp, vp,
+                                                   ctypes.POINTER(sz), vp]
     lib.sift_hip_detect_batch.argtypes = [vp, ctypes.POINTER(vp), i, i, i, i, i,
                                           ctypes.POINTER(CParams), ctypes.POINTER(vp),
                                           ctypes.POINTER(sz), ctypes.POINTER(vp)]
@@ -252,6 +267,61 @@ def _as_hwc(img: np.ndarray):
     if a.ndim == 3:
         return a, a.shape[1], a.shape[0], a.shape[2]
     raise ValueError("image must be (H, W) or (H, W, C)")
+
+
+class Comm:
+    """A rank of the native RCCL record exchange (include/sift_hip.h
+    sift_hip_comm_*; what a C++ batch driver uses instead of
+    torch.distributed)."""
+
+    def __init__(self, handle: ctypes.c_void_p, lib):
+        self.lib, self._c = lib, handle
+
+    @staticmethod
+    def init_all(devices) -> list:
+        """One communicator per device of this process (ncclCommInitAll)."""
+        lib = load_library()
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*devices)
+        hs = (ctypes.c_void_p * n)()
+        _check(lib.sift_hip_comm_init_all(n, devs, hs))
+        return [Comm(ctypes.c_void_p(hs[k]), lib) for k in range(n)]
+
+    def rank(self):
+        r, n = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.sift_hip_comm_rank(self._c, ctypes.byref(r), ctypes.byref(n)))
+        return r.value, n.value
+
+    def allgather_records(self, d_recs: int, ids, counts, max_local: int, d_out: int,
+                          cap_out: int, stream: int = 0):
+        """Two-phase all-gather (sift_hip_allgather_records): this rank's
+        images ids[j] with counts[j] records image-major at device pointer
+        d_recs; returns (total, ids, counts) of every rank's entries (rank-
+        major, id -1 = empty); the records land at d_out rank-major."""
+        _, nranks = self.rank()
+        n_local = len(ids)
+        ids_a = np.asarray(ids, dtype=np.int64)
+        cnt_a = np.asarray(counts, dtype=np.uint64)
+        out_ids = np.empty(nranks * max_local, dtype=np.int64)
+        out_cnt = np.empty(nranks * max_local, dtype=np.uint64)
+        n_out = ctypes.c_size_t()
+        _check(self.lib.sift_hip_allgather_records(
+            self._c, ctypes.c_void_p(d_recs or None), ids_a.ctypes.data if n_local else None,
+            cnt_a.ctypes.data if n_local else None, n_local, max_local,
+            ctypes.c_void_p(d_out or None), cap_out, out_ids.ctypes.data, out_cnt.ctypes.data,
+            ctypes.byref(n_out), ctypes.c_void_p(stream or None)))
+        return n_out.value, out_ids, out_cnt
+
+    def close(self) -> None:
+        if self._c:
+            self.lib.sift_hip_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:

@@ -53,7 +53,7 @@ def test_params_default_are_reference_defaults():
 
 def test_strerror_covers_codes():
     lib = load_library()
-    for code in range(0, -9, -1):
+    for code in range(0, -10, -1):
         assert lib.sift_hip_strerror(code).decode() != "unknown error"
 
 
@@ -115,6 +115,38 @@ def test_host_u8_packing_pass():
                 b = img.copy()
                 b[pos] = bad
                 assert not f(b.ctypes.data, n, out.ctypes.data), (n, bad, pos)
+
+
+def test_host_pack_pool_generations():
+    """the pooled pack pass tags task claims with their
+    generation, so back-to-back calls of different task counts (images of
+    different sizes above 2^17 elements) never run or count another call's
+    tasks. Many alternating calls, every result checked."""
+    import numpy as np
+
+    lib = load_library()
+    f = lib._ZN8sift_amd12host_pack_u8EPKdmPh
+    f.restype = ctypes.c_bool
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    rng = np.random.default_rng(11)
+    sizes = [(1 << 17) * k + 3 for k in (2, 9, 3, 17, 5)]
+    imgs = {n: rng.integers(0, 256, size=n).astype(np.float64) for n in sizes}
+    for it in range(300):
+        n = sizes[it % len(sizes)]
+        out = np.zeros(n, np.uint8)
+        assert f(imgs[n].ctypes.data, n, out.ctypes.data)
+        assert np.array_equal(out, imgs[n].astype(np.uint8)), (it, n)
+
+
+def test_comm_entry_points_reject_bad_args_without_gpu():
+    """The native RCCL exchange's argument checks need no device."""
+    lib = load_library()
+    assert lib.sift_hip_comm_init_all(0, None, None) == -1
+    assert lib.sift_hip_comm_destroy(None) == -1
+    assert lib.sift_hip_comm_rank(None, None, None) == -1
+    n = ctypes.c_size_t()
+    assert lib.sift_hip_allgather_records(None, None, None, None, 0, 1, None, 0, None, None,
+                                          ctypes.byref(n), None) == -1
 
 
 def test_python_binding_argument_counts_match_the_header():
