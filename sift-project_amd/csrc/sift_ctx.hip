@@ -53,6 +53,9 @@ namespace {
 
 using clk = std::chrono::steady_clock;
 
+constexpr unsigned kKpWgsMax = 512;               // keypoint workgroups per launch, at most
+constexpr size_t kTileMaxPx = (size_t)1 << 21;    // planes up to this size: LDS-tile blur
+
 // Keypoint lanes: batches alternate between two streams (C, D), each with
 // its own region of every keypoint array and its own counters, so the chains
 // of consecutive batches run concurrently (within a lane they are serial and
@@ -160,19 +163,6 @@ struct EventPair {
 
 enum SlotState { kFree = 0, kSubmitted = 1, kFinalized = 2 };
 
-// Everything a job's stream work depends on: its shape and parameters, its
-// inputs (device pointers; host bytes go through the slot's pinned staging)
-// and the slot's buffers (grow-only: same pointers and capacities). Not the
-// stream: a graph is launched on whichever stream the job was given.
-// Compared bytewise (zero-initialised, so padding is zero).
-struct GraphKey {
-    int n_img, kind, w, h, c, want_df;
-    sift_params p;
-    const void* img[SIFT_MAX_BATCH];
-    const void* buf[12];
-    size_t cap[6];
-};
-
 // Everything one job owns; reused (grow-only) by later jobs in this slot.
 struct Slot {
     int state = kFree;
@@ -195,7 +185,6 @@ struct Slot {
     DevBuf<sift_kp> ori;
     DevBuf<RecSide> side;
     DevBuf<float> df32;
-    DevBuf<unsigned> lab;  // SIFT_LAB_DOUBLE: counters of the duplicate launches
     size_t cap_cand = 0, cap_raw = 0, cap_ori = 0;  // per lane
     unsigned* d_ctr = nullptr;
     unsigned* h_ctr = nullptr;  // pinned, live counters of every lane
@@ -219,21 +208,7 @@ struct Slot {
     // slot's pair)
     hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
     int lanes = kLanes;
-    int o_big = 0;  // octaves below: wavefront-per-keypoint kernels (enqueue_job)
     std::vector<EventPair> pending;
-    // launch graph of this slot's job (enqueue_job_graph): valid while the
-    // key (job shape, streams, inputs, buffer state) repeats
-    GraphKey gkey{};
-    bool gvalid = false;
-    // the job as graph segments, each followed by the event that ends it
-    // (chain ends, done): events are recorded between segment launches,
-    // since HIP rejects event records captured into a graph
-    std::vector<hipGraphExec_t> gseg;
-    std::vector<hipEvent_t> gseg_ev;
-    int g_nchains = 0;
-    std::vector<int> g_chain_lane;
-    bool capturing = false;
-    hipStream_t capture_stream = nullptr;
     // finalize
     bool exported = true;
     unsigned n_lane[kLanes] = {};
@@ -266,25 +241,17 @@ struct sift_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // = pyr_stream[0]: the public stream (matcher)
     // persistent workgroups of orientation / descriptor per launch, per
-    // image of the job (capped at kp_wgs_max): four keypoints in flight per
-    // workgroup. Fewer than the chip could hold, deliberately: the keypoint
-    // kernels are gather-latency-bound, and in the pipelined steady state
-    // their resident waves take register file and memory bandwidth from the
-    // other jobs' blurs. Interleaved A/B on 1080p, single-image jobs (four in
-    // flight): 192 per image 0.521 ms, 256 0.527, 512 0.548; 8-image jobs
-    // want 512 in all (0.503 ms per image vs 0.537 at 1024, 0.516 at 768). SIFT_KP_WGS,
-    // SIFT_DESC_WGS, SIFT_KP_WGS_MAX
+    // image of the job (capped at kKpWgsMax). Fewer than the chip could
+    // hold, deliberately: the keypoint kernels are gather-latency-bound, and
+    // in the pipelined steady state their resident waves take register file
+    // and memory bandwidth from the other jobs' blurs (round 3, interleaved
+    // A/B on 1080p, single-image jobs four in flight: 192 per image 0.521
+    // ms, 256 0.527, 512 0.548; 8-image jobs 0.503 ms per image at 512 in
+    // all vs 0.537 at 1024). A job alone on the chip gets the same grid:
+    // 1024 workgroups starved the concurrent small-octave blurs on its
+    // critical path. SIFT_KP_WGS / SIFT_DESC_WGS (tuning).
     unsigned kp_wgs = 192;
     unsigned desc_wgs = 192;
-    unsigned kp_wgs_max = 512;
-    unsigned kp_wgs_small = 512;   // SIFT_KP_WGS_SMALL: workgroup-per-keypoint chains
-    // a job alone on the chip (two keypoint lanes): per image, 0 = kp_wgs /
-    // desc_wgs (SIFT_KP_WGS_ALONE)
-    unsigned kp_wgs_alone = 0;
-    // octaves of fewer pixels per image use the workgroup-per-keypoint
-    // orientation / descriptor kernels (SIFT_KP_SMALL_PX; 0: never). Off:
-    // at 2^20 (1080p octaves >= 2) the extra chain cost 3.6 % pipelined
-    size_t kp_small_px = 0;
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
     // rest form one final batch after the LDS octaves. A single-image job
     // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
@@ -292,63 +259,42 @@ struct sift_ctx {
     // Jobs alone on all four streams and multi-image jobs keep 2^18: the
     // batches overlap the smaller octaves' pyramid (2^22 raised the
     // synchronous latency from 0.90 to 1.25 ms and 8-image jobs by 4 %;
-    // profiles/r02_ab/r02ap, r02as)
+    // profiles/r02_ab/r02ap, r02as). SIFT_BATCH_PX_LOG2 (tests).
     int batch_px_log2 = 22;
     int batch_px_log2_alone = 18;
-    size_t tile_max_px = (size_t)1 << 21;  // planes up to this size: LDS-tile blur
     // octaves of at most this many pixels (and within the LDS, lds_octave_fits)
-    // run LDS-resident in the one-workgroup k_octaves_lds (SIFT_LDS_PX)
+    // run LDS-resident in the one-workgroup k_octaves_lds (SIFT_LDS_PX, tests)
     size_t lds_max_px = kLdsOctavePx;
-    bool shared_streams = false;  // SIFT_SHARED_STREAMS=1: every job on all four streams
-    bool serial = false;          // SIFT_SERIAL=1: every kernel on one stream (profiling)
-    // SIFT_LAB_DOUBLE (lab measurement only): every launch of the selected
-    // kernel families runs twice, the duplicate with its outputs discarded
-    // (capacity 0, scratch counters) or idempotent (blurs, descriptor bytes);
-    // the pipelined time difference is the family's marginal cost. Bits:
-    // 1 strip blurs (planes > tile_max_px), 32 tile blurs, 64 LDS octaves,
-    // 2 extrema, 4 refine, 8 orientation, 16 descriptor
-    unsigned lab_double = 0;
-    bool extrema_stream = true;   // SIFT_EXTREMA_TILES=1: the LDS-tile extrema kernel
-    bool fuse_initial = true;     // SIFT_FUSE_INITIAL=0: gray/x2 in k_prepare, then blur (A/B)
-    bool job_pairs = false;       // SIFT_JOB_STREAMS=2: two streams per job beyond the first
-    // SIFT_STREAM_POLICY (default 2). 0 = round 2: a job alone takes all
-    // four pair streams, next to one other a free pair, else one free stream
-    // (pair streams first). 2 = a caller seen pipelining (pipe_hint: a job
-    // submitted next to another in the last kPipeHint submits) gets one
-    // stream per job, pair streams first, even when its pipeline is
-    // momentarily empty, so the next jobs of a burst do not share the first
-    // job's hardware queues. 1 = the same from the normal-priority pool
-    // first; 3 = from four high-priority streams. HIP pools hardware queues
-    // per stream priority (high: -1; normal: 0, shared with every default
-    // stream of the process, torch's included). Measured with the driver's
-    // bench command (20 steps, four in flight; profiles/r03_i): policy 2
-    // 0.586-0.593 ms per step, 0 0.582-0.640, 1 0.72 (normal pool shared
-    // with torch), 3 0.72-0.77 (four equal priorities: the four jobs in
-    // flight progress together and finish together, so the host waits a
-    // whole job latency every fourth step and refills in bursts)
-    int stream_policy = 2;
-    // SIFT_GRAPHS=1: pipelined jobs through per-slot launch graphs
-    // (enqueue_job_graph). Off by default: the host's enqueue drops from
-    // 0.12 to 0.03-0.04 ms per 1080p job, but the driver's bench command ran
-    // 0.596 / 0.610 ms per step against 0.584 / 0.590 eager (the host is not
-    // the bottleneck at four jobs in flight; profiles/r03_j)
-    bool graphs = false;
-    // SIFT_AGE_PRIO (A/B knob): kernels raise their waves' issue priority by
-    // their job's age rank (JobPrio); d_done counts the context's completed
-    // jobs (k_job_done at the end of every job)
-    bool age_prio = true;
+    bool serial = false;  // SIFT_SERIAL=1: every kernel on one stream (profiling)
+    // Kernels raise their waves' issue priority by their job's age rank
+    // (JobPrio; -1.3 % on the driver's bench command, round 3); d_done
+    // counts the context's completed jobs (k_job_done at the end of every
+    // job)
     unsigned* d_done = nullptr;
     unsigned prio_seq = 0;  // jobs whose k_job_done was enqueued (JobPrio.ticket)
     DevBuf<unsigned long long> verify_acc;  // sift_hip_verify_slots: per-slot sums
     hipEvent_t verify_ev = nullptr;         // the last verify_slots call's end
     bool verify_used = false;
+    // Streams of a job (submit_impl): a caller seen pipelining (pipe_hint:
+    // a job submitted next to another in the last kPipeHint submits) gets one
+    // stream per job, the pair streams first, even when its pipeline is
+    // momentarily empty, so the next jobs of a burst do not share the first
+    // job's hardware queues; a job alone takes all four pair streams, next
+    // to one other job a free pair. HIP pools hardware queues per stream
+    // priority (high: -1; normal: 0, shared with every default stream of the
+    // process, torch's included). Round 3 on the driver's bench command (20
+    // steps, four in flight; profiles/r03_i): this policy 0.586-0.593 ms per
+    // step; the round-2 policy (one stream per job only while others are in
+    // flight) 0.582-0.640; normal-priority streams first 0.72 (the pool is
+    // shared with torch); four equal high-priority streams 0.72-0.77 (the
+    // jobs in flight progress and finish together, the host refills in
+    // bursts). Launch graphs per slot cut the host's enqueue from 0.12 to
+    // 0.03 ms per job but ran the step 2 % slower (profiles/r03_j): removed.
     int pipe_hint = 0;
-    int ori_mode = 1;             // SIFT_ORI_MODE: 1 wave per keypoint, 0 workgroup per keypoint
     // SIFT_DESC_MODE: 0 = k_descriptor_split, f64 sample math (default, the
     // reference's arithmetic); A/B only: 1 = k_descriptor_wave (f32 sample
     // math, a wavefront per record), 2 = k_descriptor_split with f32 math
     int desc_mode = 0;
-    int lanes = kLanes;      // 1: every batch on C (SIFT_KP_LANES=1, for A/B)
     Slot slots[kSlots];
     // two stream pairs, one per hardware queue each (HIP's default is four
     // queues per process): pair k = pyramid (high priority) + keypoint chains
@@ -432,28 +378,19 @@ int prof_events(sift_ctx* ctx, Slot& s, hipEvent_t* e0, hipEvent_t* e1, double b
     return SIFT_OK;
 }
 
-// task table of one extrema launch over octaves [o_begin, o_end): tiles of
-// 64 x 16 centres (k_extrema_tiles) or strips of kExtSpan columns x kExtSeg
-// rows (k_extrema_stream)
-ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img, bool stream) {
+// task table of one k_extrema_stream launch over octaves [o_begin, o_end):
+// strips of kExtSpan centre columns x segments of centre rows
+ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img) {
     ExtremaGrid eg;
     std::memset(&eg, 0, sizeof eg);
-    const int cw = stream ? kExtSpan : 64;
     for (int o = o_begin; o < o_end; ++o) {
         const int i = eg.n++;
-        const int tx = g.W[o] > 2 ? (g.W[o] - 2 + cw - 1) / cw : 0;
-        // streaming: segments short enough for ~4096 waves per octave over
-        // the job (the small octaves are latency-bound), at least 4 rows
-        // (2 priming rows per segment), at most 64
-        int ch = 16;
-        if (stream) {
-            static const long waves = [] {  // SIFT_EXT_WAVES: A/B knob
-                const char* e = std::getenv("SIFT_EXT_WAVES");
-                return e ? std::max(64L, std::atol(e)) : 4096L;
-            }();
-            const long rows = (long)tx * std::max(g.H[o] - 2, 0) * n_img / waves;
-            ch = (int)std::min<long>(64, std::max<long>(4, rows));
-        }
+        const int tx = g.W[o] > 2 ? (g.W[o] - 2 + kExtSpan - 1) / kExtSpan : 0;
+        // segments short enough for ~4096 waves per octave over the job (the
+        // small octaves are latency-bound; 3072 / 6144 / 12288 measured
+        // within 1 %), at least 4 rows (2 priming rows per segment), at most 64
+        const long rows = (long)tx * std::max(g.H[o] - 2, 0) * n_img / 4096L;
+        const int ch = (int)std::min<long>(64, std::max<long>(4, rows));
         const int ty = g.H[o] > 2 ? (g.H[o] - 2 + ch - 1) / ch : 0;
         eg.oct[i] = o;
         eg.tiles_x[i] = tx > 0 ? tx : 1;
@@ -463,10 +400,14 @@ ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img, b
     return eg;
 }
 
-hipError_t launch_extrema_set(const sift_ctx* ctx, const PyrTable* d_pt, const Geometry& g,
-                              int o_begin, int o_end, int n_img, int thr, sift_extremum* cand,
-                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s,
-                              hipEvent_t e0, hipEvent_t e1);
+hipError_t launch_extrema_set(const PyrTable* d_pt, const Geometry& g, int o_begin, int o_end,
+                              int n_img, int thr, sift_extremum* cand, unsigned* counter,
+                              unsigned cap, unsigned* snap, hipStream_t s, hipEvent_t e0,
+                              hipEvent_t e1) {
+    const ExtremaGrid eg = extrema_grid(g, o_begin, o_end, n_img);
+    return launch_extrema_stream(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s, e0,
+                                 e1);
+}
 
 // keypoint-array capacities of a slot (per lane), all size_t and bounded so
 // that the kernels' 32-bit indices and the df32 product never wrap
@@ -497,36 +438,6 @@ void abandon(sift_ctx* ctx, Slot& s) {
     s.ticket = -1;
 }
 
-// Record `e` on stream `st`. While a job is being captured (enqueue_job_graph)
-// this ends the current graph segment, launches it, records the event
-// eagerly and begins the next segment.
-hipError_t record_event(Slot& s, hipEvent_t e, hipStream_t st) {
-    if (!s.capturing) return hipEventRecord(e, st);
-    hipGraph_t graph = nullptr;
-    hipError_t r = hipStreamEndCapture(s.capture_stream, &graph);
-    hipGraphExec_t exec = nullptr;
-    if (r == hipSuccess) r = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    if (graph) (void)hipGraphDestroy(graph);
-    if (r != hipSuccess) {
-        s.capturing = false;
-        return r;
-    }
-    s.gseg.push_back(exec);
-    s.gseg_ev.push_back(e);
-    if ((r = hipGraphLaunch(exec, s.capture_stream)) != hipSuccess ||
-        (r = hipEventRecord(e, s.capture_stream)) != hipSuccess ||
-        (r = hipStreamBeginCapture(s.capture_stream, hipStreamCaptureModeRelaxed)) != hipSuccess)
-        s.capturing = false;
-    return r;
-}
-
-void drop_graph(Slot& s) {
-    for (hipGraphExec_t x : s.gseg) (void)hipGraphExecDestroy(x);
-    s.gseg.clear();
-    s.gseg_ev.clear();
-    s.gvalid = false;
-}
-
 // One keypoint chain: extrema over octaves [o_begin, o_end) -> refine ->
 // orientation -> descriptor, on lane `lane`'s arrays and live counters, on
 // stream sx. `begin` (the snapshot written by the extrema launch's last
@@ -539,7 +450,6 @@ struct ChainSpec {
     unsigned* begin;
     hipStream_t sx;
     unsigned* work;  // orientation / descriptor work counters (work, work + 2)
-    unsigned* lab;   // SIFT_LAB_DOUBLE: 8 scratch counters, or nullptr
     ExportSink ex;
 };
 
@@ -555,7 +465,6 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     unsigned* const begin = c.begin;
     const unsigned* const cand_begin = c.cand_begin;
     unsigned* const work = c.work;
-    unsigned* const lab = c.lab;
     unsigned* live = s.d_ctr + 4 * L;
     sift_extremum* cand = s.cand.p + (size_t)L * s.cap_cand;
     RawKp* raw = s.raw.p + (size_t)L * s.cap_raw;
@@ -569,7 +478,7 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
         hipEvent_t e0, e1;
         if (prof_events(ctx, s, &e0, &e1, xb * n_img, SIFT_PROF_EXTREMA) != SIFT_OK)
             return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold, cand,
+        SIFT_HIP_TRY(launch_extrema_set(d_pt, g, o_begin, o_end, n_img, dp.threshold, cand,
                                         live + 0, cap_cand, begin, sx, e0, e1));
     } else {
         for (int o = o_begin; o < o_end; ++o)
@@ -579,25 +488,9 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
         if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 3));
     }
     const unsigned* b = begin ? begin : zeros;
-    // keypoint kernel flavour (octaves below o_big: wavefront per keypoint)
-    // and persistent grid of this chain (kp_wgs per image, also for a job
-    // alone on the chip: with 1024 workgroups the keypoint waves starved the
-    // concurrent small-octave blurs on the critical path, 1.03 vs 0.95 ms)
-    const bool small = o_begin >= s.o_big;
-    const int ori_mode = (small && ctx->ori_mode == 1) ? 0 : ctx->ori_mode;
-    const int desc_mode = ctx->desc_mode;
-    const bool alone = s.lanes > 1 && ctx->kp_wgs_alone;
-    unsigned ori_wgs = std::min(ctx->kp_wgs_max,
-                                (alone ? ctx->kp_wgs_alone : ctx->kp_wgs) * (unsigned)n_img);
-    unsigned desc_wgs = std::min(ctx->kp_wgs_max,
-                                 (alone ? ctx->kp_wgs_alone : ctx->desc_wgs) * (unsigned)n_img);
-    if (small) ori_wgs = desc_wgs = ctx->kp_wgs_small;
-    if (lab) {
-        SIFT_HIP_TRY(hipMemsetAsync(lab, 0, 8 * sizeof(unsigned), sx));
-        if (ctx->lab_double & 2u)
-            SIFT_HIP_TRY(launch_extrema_set(ctx, d_pt, g, o_begin, o_end, n_img, dp.threshold,
-                                            cand, lab, 0, nullptr, sx, nullptr, nullptr));
-    }
+    // persistent grid of this chain: kp_wgs / desc_wgs per image
+    const unsigned ori_wgs = std::min(kKpWgsMax, ctx->kp_wgs * (unsigned)n_img);
+    const unsigned desc_wgs = std::min(kKpWgsMax, ctx->desc_wgs * (unsigned)n_img);
     hipEvent_t r0, r1, q0, q1, d0, d1;  // profiling events of the keypoint stages
     if (prof_events(ctx, s, &r0, &r1, 0.0, SIFT_PROF_REFINE) != SIFT_OK ||
         prof_events(ctx, s, &q0, &q1, 0.0, SIFT_PROF_ORIENT) != SIFT_OK ||
@@ -605,20 +498,10 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
         return SIFT_ERR_HIP;
     SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
                                raw, live + 1, cap_raw, sx, r0, r1));
-    if (lab && (ctx->lab_double & 4u))
-        SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0,
-                                   cap_cand, raw, lab + 1, 0, sx));
     SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
-                               cap_ori, work, ori_wgs, ori_mode, sx, q0, q1));
-    if (lab && (ctx->lab_double & 8u))
-        SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, lab + 2,
-                                   0, lab + 3, ori_wgs, ori_mode, sx));
+                               cap_ori, work, ori_wgs, sx, q0, q1));
     SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
-                                   work + 2, c.ex, desc_wgs, desc_mode, sx, d0, d1));
-    if (lab && (ctx->lab_double & 16u))
-        SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, nullptr,
-                                       lab + 4, ExportSink{nullptr, nullptr, nullptr, 0},
-                                       desc_wgs, desc_mode, sx));
+                                   work + 2, c.ex, desc_wgs, ctx->desc_mode, sx, d0, d1));
     return SIFT_OK;
 }
 
@@ -738,10 +621,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         double* decp = dec ? s.h_pt.lvl[o + 1][0] : nullptr;
         double* tmp = wide ? s.tmp.p + (o & 1) * tmp_half : nullptr;
         SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp, so,
-                                 e0, e1, ctx->tile_max_px));
-        if (ctx->lab_double & ((size_t)W * H > ctx->tile_max_px ? 1u : 32u))
-            SIFT_HIP_TRY(launch_blur(bsrc, src_bs, dst, stride, n_img, W, H, t, decp, Wd, Hd, tmp,
-                                     so, nullptr, nullptr, ctx->tile_max_px));
+                                 e0, e1, kTileMaxPx));
         return SIFT_OK;
     };
 
@@ -753,8 +633,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             SIFT_OK)
             return SIFT_ERR_HIP;
         hipError_t err = hipSuccess;
-        const bool fused = ctx->fuse_initial &&
-                           launch_blur_initial_fused(src, in_bs, s.w, s.h, s.c,
+        const bool fused = launch_blur_initial_fused(src, in_bs, s.w, s.h, s.c,
                                                      p->double_image_size ? 1 : 0,
                                                      s.h_pt.lvl[0][0], stride, n_img, W0, H0,
                                                      s.taps_init, sA, e0, e1, &err);
@@ -801,23 +680,6 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             break;
         }
     o_merge = std::min(o_merge, o_small);
-    // octaves [0, o_big) have at least kp_small_px pixels per image: their
-    // keypoints go through the wavefront-per-keypoint orientation /
-    // descriptor kernels, the smaller octaves' through the workgroup-per-
-    // keypoint ones (four waves per keypoint shorten the latency of each,
-    // which is what a launch over few keypoints is made of). A chain never
-    // mixes the two: the two flavours sum histograms in different orders, and
-    // a keypoint's records must not depend on how its job was batched. So
-    // octaves [o_merge, o_mid) form a chain of their own, enqueued after
-    // octave o_mid - 1, and the final chain starts at max(o_merge, o_mid).
-    // (kp_small_px 0, the default: every octave takes the wavefront kernels
-    // and there is no mid chain)
-    int o_big = 0;
-    while (o_big < g.octaves && (double)g.W[o_big] * g.H[o_big] >= (double)ctx->kp_small_px)
-        ++o_big;
-    if (o_big >= o_small) o_big = g.octaves;
-    const int o_mid = o_big == g.octaves ? o_merge : std::max(o_big, o_merge);
-    const int o_fin = o_mid;
     const unsigned* zeros = s.d_ctr + kCtrZeros;
     auto snap = [&](int gb) { return s.d_ctr + kCtrSnap + 4 * gb; };
     // records of every chain also go to the mapped export buffers, sized from
@@ -833,7 +695,6 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // lane L exports its records (lane-local index i) to exp_rec[L * exp_lane + i]
     s.exp_lane = s.exp_rec.cap / kLanes;
 
-    s.o_big = o_big;
     auto run_chain = [&](int L, int o_begin, int o_end, const unsigned* cand_begin,
                          unsigned* begin) -> int {
         const int ci = s.n_chains++;
@@ -844,18 +705,13 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 return SIFT_ERR_HIP;
             s.chain_ev.push_back(e);
         }
-        unsigned* lab = nullptr;  // 8 scratch counters of this chain's duplicates
-        if (ctx->lab_double & 30u) {
-            if ((st = s.lab.ensure(8 * (kMaxOctaves + 2))) != SIFT_OK) return st;
-            lab = s.lab.p + 8 * ci;
-        }
         const ChainSpec c{L, o_begin, o_end, cand_begin, begin, lane_stream[L],
-                          s.d_ctr + kCtrWork + 4 * ci, lab,
+                          s.d_ctr + kCtrWork + 4 * ci,
                           ExportSink{s.exp_rec.d + (size_t)L * s.exp_lane,
                                      s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
                                      (unsigned)s.exp_lane}};
         if ((st = enqueue_chain(ctx, s, c)) != SIFT_OK) return st;
-        SIFT_HIP_TRY(record_event(s, s.chain_ev[ci], c.sx));
+        SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], c.sx));
         return SIFT_OK;
     };
     int n_batches = 0;
@@ -902,8 +758,6 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             }
         }
         if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
-        if (o + 1 == o_mid && o_merge < o_mid && (st = batch(o_merge, o_mid, {sA, sB})) != SIFT_OK)
-            return st;
     }
     if (o_small < g.octaves) {
         hipStream_t so = pyr[o_small & 1];
@@ -918,11 +772,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss, s.d_stage->taps,
                                         n_img, so, e0, e1));
-        if (ctx->lab_double & 64u)
-            SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss,
-                                            s.d_stage->taps, n_img, so, nullptr, nullptr));
     }
-    if (o_fin < g.octaves && (st = batch(o_fin, g.octaves, {sA, sB})) != SIFT_OK) return st;
+    if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
     // lane D joins C, then the live counters come back on C: the job's last
     // device work (the final batch waited on both pyramid streams)
     if (sD != sC) {
@@ -937,132 +788,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     }
     SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                 hipMemcpyDeviceToHost, sC));
-    SIFT_HIP_TRY(record_event(s, s.done_ev, sC));
+    SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
     s.t_host[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-    return SIFT_OK;
-}
-
-// Every buffer enqueue_job grows, sized up front with the same requests, so
-// that a job's enqueue allocates nothing (graph capture: enqueue_job_graph).
-int prepare_buffers(Slot& s, int kind) {
-    const Geometry& g = s.g;
-    const int n_img = s.n_img;
-    const size_t ne = (size_t)s.w * s.h * s.c;
-    int st;
-    if (!(kind == SIFT_INPUT_F64_DEVICE && n_img == 1)) {
-        if ((st = s.in.ensure(ne * n_img)) != SIFT_OK) return st;
-        if (kind == SIFT_INPUT_F64_HOST || kind == SIFT_INPUT_U8_HOST) {
-            if ((st = s.h_up.ensure(ne * n_img * sizeof(double))) != SIFT_OK) return st;
-            if ((st = s.in8.ensure(ne * n_img)) != SIFT_OK) return st;
-        }
-    }
-    if ((st = s.pyr.ensure(g.total * n_img)) != SIFT_OK) return st;
-    bool wide = s.taps_init.R > kMaxTemplR || s.taps_init.R < 1;
-    for (int l = 1; l < g.n_gauss; ++l) wide |= s.taps[l].R > kMaxTemplR || s.taps[l].R < 1;
-    if (wide && (st = s.tmp.ensure(2 * (size_t)g.W[0] * g.H[0] * n_img)) != SIFT_OK) return st;
-    const size_t want_cand =
-        std::min<size_t>(std::max<size_t>(g.sum_px * n_img / 32, 65536), kMaxCand);
-    if ((st = ensure_kp_arrays(s, std::max(s.cap_cand, want_cand), std::max(s.cap_raw, want_cand),
-                               std::max(s.cap_ori, 2 * want_cand))) != SIFT_OK)
-        return st;
-    const size_t exp_want = std::max<size_t>(s.exp_rec.cap, (size_t)8192 * n_img * kLanes);
-    if ((st = s.exp_rec.ensure(exp_want)) != SIFT_OK ||
-        (st = s.exp_side.ensure(s.exp_rec.cap)) != SIFT_OK ||
-        (st = s.exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
-        return st;
-    return SIFT_OK;
-}
-
-GraphKey graph_key(const Slot& s, const void* const* images, int kind) {
-    GraphKey k;
-    std::memset(&k, 0, sizeof k);
-    k.n_img = s.n_img;
-    k.kind = kind;
-    k.w = s.w;
-    k.h = s.h;
-    k.c = s.c;
-    k.want_df = s.want_df;
-    k.p = s.p;
-    const bool dev = kind == SIFT_INPUT_F64_DEVICE || kind == SIFT_INPUT_U8_DEVICE;
-    for (int b = 0; b < s.n_img && dev; ++b) k.img[b] = images[b];
-    const void* buf[12] = {s.in.p, s.in8.p, s.pyr.p, s.tmp.p, s.cand.p, s.raw.p,
-                           s.ori.p, s.side.p, s.df32.p, s.exp_rec.d, s.exp_side.d, s.h_up.p};
-    std::memcpy(k.buf, buf, sizeof buf);
-    const size_t cap[6] = {s.cap_cand, s.cap_raw, s.cap_ori, s.exp_rec.cap, s.exp_cnt.cap,
-                           s.h_up.cap};
-    std::memcpy(k.cap, cap, sizeof cap);
-    return k;
-}
-
-// A job's launches through a per-slot hipGraph: the host cost of ~38
-// launches and copies (0.11-0.15 ms per 1080p job) becomes one graph launch.
-// Single-stream jobs only (the pipelined case; a job alone on the chip runs
-// its pyramid octaves and keypoint lanes on four streams, eagerly), device
-// or byte inputs (a host Image of doubles may or may not pack to bytes),
-// never with profiling events or lab knobs. prepare_buffers sizes every
-// buffer first, so the capture allocates nothing; a job whose key matches
-// the slot's graph replays it, another captures its own. A replay repeats only the host side of
-// enqueue_job: the input bytes for host images and the export poison.
-int enqueue_job_graph(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
-    const bool single = s.sA == s.sB && s.sA == s.sC && s.sA == s.sD;
-    int st = prepare_buffers(s, kind);
-    if (st != SIFT_OK) return st;
-    const GraphKey key = graph_key(s, images, kind);
-    const bool match = s.gvalid && std::memcmp(&key, &s.gkey, sizeof key) == 0;
-    if (!ctx->graphs || !single || ctx->profiling || ctx->lab_double ||
-        kind == SIFT_INPUT_F64_HOST) {
-        // an eager job of another key rewrites the slot's host staging (the
-        // pyramid table the graph's first copy uploads): the graph is stale
-        if (!match) s.gvalid = false;
-        return enqueue_job(ctx, s, images, kind);
-    }
-    hipStream_t stream = s.sA;
-    if (match) {
-        const auto t0 = clk::now();
-        s.t_submit = t0;
-        s.ev_i = 0;
-        s.ev_used = 0;
-        s.pending.clear();
-        s.n_chains = s.g_nchains;
-        s.chain_lane = s.g_chain_lane;
-        if (kind == SIFT_INPUT_U8_HOST) {  // the staging the graph's first copy reads
-            const size_t ne = (size_t)s.w * s.h * s.c;
-            for (int b = 0; b < s.n_img; ++b) std::memcpy(s.h_up.p + b * ne, images[b], ne);
-        }
-        std::fill(s.exp_cnt.h, s.exp_cnt.h + s.exp_cnt.cap, 0xFFFFFFFFu);
-        for (size_t i = 0; i < s.gseg.size(); ++i) {
-            SIFT_HIP_TRY(hipGraphLaunch(s.gseg[i], stream));
-            SIFT_HIP_TRY(hipEventRecord(s.gseg_ev[i], stream));
-        }
-        s.t_host[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-        return SIFT_OK;
-    }
-    // capture this job's launches segment by segment (record_event launches
-    // each segment as it closes), keep the segments for the next jobs
-    drop_graph(s);
-    SIFT_HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
-    s.capturing = true;
-    s.capture_stream = stream;
-    st = enqueue_job(ctx, s, images, kind);
-    const bool ok = s.capturing;  // false: a segment failed (capture ended)
-    s.capturing = false;
-    if (ok) {  // the empty capture after the last event
-        hipGraph_t graph = nullptr;
-        const hipError_t ce = hipStreamEndCapture(stream, &graph);
-        if (graph) (void)hipGraphDestroy(graph);
-        if (st == SIFT_OK && ce != hipSuccess) st = SIFT_ERR_HIP;
-    } else if (st == SIFT_OK) {
-        st = SIFT_ERR_HIP;
-    }
-    if (st != SIFT_OK) {
-        drop_graph(s);
-        if (debug_enabled()) std::fprintf(stderr, "sift_hip: graph capture failed (%d)\n", st);
-        return st;
-    }
-    s.gkey = key;
-    s.gvalid = true;
-    s.g_nchains = s.n_chains;
-    s.g_chain_lane = s.chain_lane;
     return SIFT_OK;
 }
 
@@ -1116,20 +843,16 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
             SIFT_HIP_TRY(hipMemsetAsync(s.d_ctr, 0, kCtrWords * sizeof(unsigned), sC));
             s.n_chains = 0;
             s.chain_lane.clear();
-            // every octave again on lane 0, as two chains split at the kernel
-            // flavour boundary o_big (records as a normal run's); no export
-            const int ranges[3] = {0, std::min(s.o_big, g.octaves), g.octaves};
-            const unsigned* cb = s.d_ctr + kCtrZeros;
-            for (int r = 0; r < 2; ++r) {
-                if (ranges[r] >= ranges[r + 1]) continue;
-                unsigned* begin = s.d_ctr + kCtrSnap + 4 * s.n_chains;
-                const ChainSpec c{0, ranges[r], ranges[r + 1], cb, begin, sC,
-                                  s.d_ctr + kCtrWork + 4 * s.n_chains, nullptr,
+            // every octave again as one chain on lane 0 (a keypoint's
+            // records do not depend on its chain); no export
+            {
+                unsigned* begin = s.d_ctr + kCtrSnap;
+                const ChainSpec c{0, 0, g.octaves, s.d_ctr + kCtrZeros, begin, sC,
+                                  s.d_ctr + kCtrWork,
                                   ExportSink{s.exp_rec.d, s.exp_side.d, nullptr, 0}};
-                s.n_chains++;
+                s.n_chains = 1;
                 s.chain_lane.push_back(0);
                 if ((st = enqueue_chain(ctx, s, c)) != SIFT_OK) return st;
-                cb = begin;
             }
             SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
@@ -1249,21 +972,6 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     return SIFT_OK;
 }
 
-hipError_t launch_extrema_set(const sift_ctx* ctx, const PyrTable* d_pt, const Geometry& g,
-                              int o_begin, int o_end, int n_img, int thr, sift_extremum* cand,
-                              unsigned* counter, unsigned cap, unsigned* snap, hipStream_t s,
-                              hipEvent_t e0, hipEvent_t e1) {
-    const ExtremaGrid eg = extrema_grid(g, o_begin, o_end, n_img, ctx->extrema_stream);
-    if (ctx->extrema_stream)
-        return launch_extrema_stream(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s,
-                                     e0, e1);
-    if (e0) (void)hipEventRecord(e0, s);
-    const hipError_t e = launch_extrema_tiles(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap,
-                                              snap, s);
-    if (e1) (void)hipEventRecord(e1, s);
-    return e;
-}
-
 Slot* slot_of(sift_ctx* ctx, int ticket) {
     for (Slot& s : ctx->slots)
         if (s.state != kFree && s.ticket == ticket) return &s;
@@ -1309,7 +1017,7 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     // age rank (JobPrio): jobs are numbered by prio_seq, which advances only
     // when a job's k_job_done was enqueued (the job will count in d_done);
     // both counters wrap together modulo 2^32
-    const JobPrio jp{(ctx->age_prio && !ctx->graphs) ? ctx->d_done : nullptr,
+    const JobPrio jp{ctx->d_done,
                      (int)(ctx->prio_seq + 1u), 0};
     s.taps_init.jp = jp;
     for (BlurTaps& t : s.taps) t.jp = jp;
@@ -1333,63 +1041,23 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
             }
         hipStream_t* q = ctx->pool;  // pyr0, pyr1, kp0, kp1, ...
         // a caller that keeps jobs in flight (pipe_hint: one submitted next
-        // to another in the last kPipeHint submits) gets one stream per job
-        // even when its pipeline is momentarily empty, so the next jobs of a
-        // burst find their hardware queues free (SIFT_STREAM_POLICY=1)
-        const bool hinted = ctx->stream_policy >= 1 && ctx->pipe_hint > 0;
+        // to another in the last kPipeHint submits) gets one stream per job,
+        // the pair streams first, even when its pipeline is momentarily
+        // empty, so the next jobs of a burst find their hardware queues free;
+        // a job alone takes all four pair streams (see sift_ctx::pipe_hint)
+        const bool hinted = ctx->pipe_hint > 0;
         if (others > 0) ctx->pipe_hint = kPipeHint;
         else if (ctx->pipe_hint > 0) --ctx->pipe_hint;
-        if (ctx->stream_policy >= 1 && (hinted || others > 0) && !ctx->shared_streams &&
-            !ctx->serial) {
-            // one stream: policy 1 from the normal-priority pool first,
-            // policy 2 from the four pair streams first; else any free one
-            int k = kSlots;
-            if (ctx->stream_policy == 3) {  // the four high-priority streams first
-                for (int c : {0, 1, 2 * kPairs, 2 * kPairs + 1})
-                    if (!(used >> c & 1u)) {
-                        k = c;
-                        break;
-                    }
-            } else {
-                k = ctx->stream_policy == 1 ? 2 * kPairs : 0;
-                while (k < kSlots && (used >> k & 1u)) ++k;
-            }
-            if (k == kSlots) {
-                k = 0;
-                while (k + 1 < kSlots && (used >> k & 1u)) ++k;
-            }
+        if (hinted || others > 0) {
+            int k = 0;
+            while (k + 1 < kSlots && (used >> k & 1u)) ++k;
             s.sA = s.sB = s.sC = s.sD = q[k];
             s.lanes = 1;
             s.uses = 1u << k;
-        } else if (others == 0 || ctx->shared_streams) {
-            s.sA = q[0], s.sB = q[1], s.sC = q[2], s.sD = q[3];
-            s.lanes = ctx->lanes;
-            s.uses = 0xFu;
-        } else if (others == 1 && !(used & 0x5u)) {
-            s.sA = s.sB = q[0], s.sC = s.sD = q[2];
-            s.lanes = 1;
-            s.uses = 0x5u;
-        } else if (others == 1 && !(used & 0xAu)) {
-            s.sA = s.sB = q[1], s.sC = s.sD = q[3];
-            s.lanes = 1;
-            s.uses = 0xAu;
         } else {
-            int k = 0;
-            if (ctx->job_pairs) {  // SIFT_JOB_STREAMS=2: a free pair (pyramid, keypoints)
-                while (k + 2 < kSlots && (used >> k & 3u)) k += 2;
-            }
-            if (ctx->job_pairs && !(used >> k & 3u) && k + 1 < kSlots) {
-                s.sA = s.sB = q[k];
-                s.sC = s.sD = q[k + 1];
-                s.lanes = 1;
-                s.uses = 3u << k;
-            } else {
-                k = 0;
-                while (k + 1 < kSlots && (used >> k & 1u)) ++k;
-                s.sA = s.sB = s.sC = s.sD = q[k];
-                s.lanes = 1;
-                s.uses = 1u << k;
-            }
+            s.sA = q[0], s.sB = q[1], s.sC = q[2], s.sD = q[3];
+            s.lanes = kLanes;
+            s.uses = 0xFu;
         }
         if (ctx->serial) {  // profiling: one stream, no overlap (kernel costs alone)
             s.sA = s.sB = s.sC = s.sD = q[0];
@@ -1411,7 +1079,7 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
     }
     s.state = kSubmitted;
     s.job_done_enqueued = false;
-    st = enqueue_job_graph(ctx, s, images, kind);
+    st = enqueue_job(ctx, s, images, kind);
     if (s.job_done_enqueued) ++ctx->prio_seq;
     if (st != SIFT_OK) {
         abandon(ctx, s);
@@ -1513,36 +1181,15 @@ int sift_hip_create(int device, sift_ctx** out) {
     ctx->device = device;
     int prio_lo = 0, prio_hi = 0;  // numerically lower = higher priority
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
-    if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::atoi(e);
-    if (ctx->kp_wgs < 1) ctx->kp_wgs = 1;
-    if (const char* e = std::getenv("SIFT_KP_WGS_MAX")) ctx->kp_wgs_max = (unsigned)std::atoi(e);
-    if (ctx->kp_wgs_max < 1) ctx->kp_wgs_max = 1;
-    if (const char* e = std::getenv("SIFT_KP_WGS_SMALL")) ctx->kp_wgs_small = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_KP_WGS_ALONE")) ctx->kp_wgs_alone = (unsigned)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_KP_SMALL_PX")) ctx->kp_small_px = (size_t)std::atoll(e);
-    if (const char* e = std::getenv("SIFT_DESC_WGS")) ctx->desc_wgs = (unsigned)std::atoi(e);
-    if (const char* e = std::getenv("SIFT_LAB_DOUBLE")) ctx->lab_double = (unsigned)std::atoi(e);
-    if (ctx->desc_wgs < 1) ctx->desc_wgs = 1;
-    if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2"))
-        ctx->batch_px_log2 = ctx->batch_px_log2_alone = std::atoi(e);
-    if (const char* e = std::getenv("SIFT_KP_LANES")) ctx->lanes = std::atoi(e) == 1 ? 1 : kLanes;
-    if (ctx->batch_px_log2 < 0 || ctx->batch_px_log2 > 40) ctx->batch_px_log2 = 22;
-    if (ctx->batch_px_log2_alone < 0 || ctx->batch_px_log2_alone > 40) ctx->batch_px_log2_alone = 18;
-    if (const char* e = std::getenv("SIFT_SHARED_STREAMS")) ctx->shared_streams = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_DESC_WGS")) ctx->desc_wgs = (unsigned)std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) {
+        const int v = std::atoi(e);
+        if (v >= 0 && v <= 40) ctx->batch_px_log2 = ctx->batch_px_log2_alone = v;
+    }
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
-    if (const char* e = std::getenv("SIFT_ORI_MODE")) ctx->ori_mode = std::atoi(e);
-    if (const char* e = std::getenv("SIFT_JOB_STREAMS")) ctx->job_pairs = std::atoi(e) == 2;
-    if (const char* e = std::getenv("SIFT_STREAM_POLICY")) ctx->stream_policy = std::atoi(e);
-    if (const char* e = std::getenv("SIFT_GRAPHS")) ctx->graphs = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SIFT_AGE_PRIO")) ctx->age_prio = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SIFT_FUSE_INITIAL")) ctx->fuse_initial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_EXTREMA_TILES")) ctx->extrema_stream = std::atoi(e) == 0;
-    if (const char* e = std::getenv("SIFT_TILE_PX_LOG2")) {
-        const int t = std::atoi(e);  // < 0: never
-        ctx->tile_max_px = t < 0 ? 0 : (size_t)1 << std::min(t, 40);
-    }
     bool ok = prepare_kernel_attributes() == hipSuccess;
     ok = ok && hipMalloc(&ctx->d_done, sizeof(unsigned)) == hipSuccess &&
          hipMemset(ctx->d_done, 0, sizeof(unsigned)) == hipSuccess;
@@ -1557,17 +1204,8 @@ int sift_hip_create(int device, sift_ctx** out) {
     ctx->pool[1] = ctx->pyr_stream[1];
     ctx->pool[2] = ctx->kp_stream[0];
     ctx->pool[3] = ctx->kp_stream[1];
-    for (int k = 2 * kPairs; k < kSlots; ++k) {
-        // policy 3: two more high-priority streams, so pipelined jobs run on
-        // four streams of equal priority (HIP pools hardware queues per
-        // priority; the normal pool is shared with every other default-
-        // priority stream of the process, torch's included)
-        if (ctx->stream_policy == 3 && k < 2 * kPairs + 2)
-            ok = ok && hipStreamCreateWithPriority(&ctx->pool[k], hipStreamNonBlocking, prio_hi) ==
-                           hipSuccess;
-        else
-            ok = ok && hipStreamCreateWithFlags(&ctx->pool[k], hipStreamNonBlocking) == hipSuccess;
-    }
+    for (int k = 2 * kPairs; k < kSlots; ++k)
+        ok = ok && hipStreamCreateWithFlags(&ctx->pool[k], hipStreamNonBlocking) == hipSuccess;
     for (Slot& s : ctx->slots) {
         ok = ok && hipMalloc(&s.d_ctr, kCtrWords * sizeof(unsigned)) == hipSuccess &&
              hipHostMalloc(&s.h_ctr, 4 * kLanes * sizeof(unsigned)) == hipSuccess &&
@@ -1602,8 +1240,6 @@ int sift_hip_destroy(sift_ctx* ctx) {
         s.ori.release();
         s.side.release();
         s.df32.release();
-        s.lab.release();
-        drop_graph(s);
         if (s.d_ctr) (void)hipFree(s.d_ctr);
         if (s.d_stage) (void)hipFree(s.d_stage);
         if (s.h_ctr) (void)hipHostFree(s.h_ctr);

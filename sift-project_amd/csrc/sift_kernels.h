@@ -43,10 +43,7 @@ hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int
 // snap (optional): the last workgroup writes the lane counter snapshot
 // (candidate end, raw / record begins) for the keypoint chain; snap[3] must
 // be zero before the launch.
-hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
-                                int n_gauss, int thr, sift_extremum* out, unsigned* counter,
-                                unsigned cap, unsigned* snap, hipStream_t s);
-// streaming variant (window_size 3): eg tasks = strips x segments per octave
+// window_size 3: eg tasks = strips x segments per octave
 hipError_t launch_extrema_stream(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
                                  int n_gauss, int thr, sift_extremum* out, unsigned* counter,
                                  unsigned cap, unsigned* snap, hipStream_t s, hipEvent_t e0,
@@ -72,7 +69,7 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
-                         unsigned* work, unsigned wgs, int mode, hipStream_t s,
+                         unsigned* work, unsigned wgs, hipStream_t s,
                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
                              const RecSide* rec_side, const unsigned* rec_begin,

@@ -720,21 +720,9 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
 // or v == min(cube): v is itself in the cube, so the centre comparison is
 // vacuous (sift.cpp:241-246). DoG values are G_{l+1} - G_l computed on the fly.
 // ---------------------------------------------------------------------------
-// Tiled variant used for window_size 3 (one launch per octave set).
-// A 256-thread workgroup owns a 64x16 block of centre pixels of one octave:
-// it stages the (66x18)-pixel DoG halo tile of every DoG layer in LDS (all
-// Gaussian loads of a thread issued before any is used, so a tile costs one
-// memory round trip), then each thread takes one column x four centre rows
-// and walks the layers with a rolling window of three layers' 3x3 max/min
-// in registers. Candidates are compacted with a 64-bit ballot per
-// (row, layer) and one atomic per wave. The last workgroup to finish takes
-// the lane's counter snapshot for the keypoint chain (snap != nullptr:
-// candidate end, raw / record begins; snap[3] is the done counter). Image b
-// of the job is blockIdx.y; candidates carry octave | b << kOctBits.
-// (Refining each candidate right here
-// was measured slower: the refine's dependent 27-point gathers serialise in
-// the tile's workgroup, where the separate thread-per-candidate k_refine
-// overlaps them across all candidates.)
+// The last workgroup of an extrema launch to finish takes the lane's counter
+// snapshot for the keypoint chain (snap != nullptr: candidate end, raw /
+// record begins; snap[3] is the done counter).
 // No memory fence here, deliberately: every candidate atomic of a workgroup
 // has returned (it is performed at the device coherence point) before the
 // workgroup's done increment, so the last workgroup's atomic reads see the
@@ -754,101 +742,6 @@ __device__ __forceinline__ void snapshot_if_last(unsigned* snap, const unsigned*
     }
 }
 
-template <int NL>
-__global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restrict__ pt,
-                                                       ExtremaGrid eg, int thr,
-                                                       sift_extremum* __restrict__ out,
-                                                       unsigned* __restrict__ counter,
-                                                       unsigned cap, unsigned* snap) {
-    constexpr int ND = NL - 1;
-    constexpr int TW = 64, TH = 16, SW = TW + 2, SH = TH + 2;
-    constexpr int NPIX = SW * SH;             // 1188 staged pixels
-    constexpr int NIT = (NPIX + 255) / 256;   // 5 per thread
-    __shared__ double sd[ND][SH][SW];
-    const int tid = threadIdx.x, lane = tid & 63;
-    int e = 0;
-    while (e + 1 < eg.n && (int)blockIdx.x >= eg.first_tile[e + 1]) ++e;
-    const int o = eg.oct[e];
-    const int b = blockIdx.y;
-    const int tile = blockIdx.x - eg.first_tile[e];
-    const int tx = tile % eg.tiles_x[e], ty = tile / eg.tiles_x[e];
-    const int W = pt->w[o], H = pt->h[o];
-    const int cx0 = 1 + tx * TW, cy0 = 1 + ty * TH;  // first centre of the tile
-    const int otag = o | (b << kOctBits);
-    {
-        double g[NIT][NL];
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int i = tid + it * 256;
-            const int r = i / SW, c = i - r * SW;
-            const size_t q = (size_t)clampi(cy0 - 1 + r, 0, H - 1) * W + clampi(cx0 - 1 + c, 0, W - 1);
-#pragma unroll
-            for (int l = 0; l < NL; ++l) g[it][l] = (i < NPIX) ? gbl(plane(pt, b, o, l))[q] : 0.0;
-        }
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int i = tid + it * 256;
-            if (i < NPIX) {
-                const int r = i / SW, c = i - r * SW;
-#pragma unroll
-                for (int l = 0; l < ND; ++l) sd[l][r][c] = g[it][l + 1] - g[it][l];
-            }
-        }
-    }
-    __syncthreads();
-    const int c = lane;              // centre column in the tile
-    const int r0 = (tid >> 6) * 4;   // first of this thread's four centre rows
-    const int x = cx0 + c;
-    const double dthr = (double)thr;
-    // rolling 3x3 max/min of layers l-2 (p), l-1 (q), l (n) for 4 centres
-    double pmx[4], pmn[4], qmx[4], qmn[4];
-#pragma unroll
-    for (int l = 0; l < ND; ++l) {
-        double rmx[6], rmn[6], nmx[4], nmn[4];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-            const double a = sd[l][r0 + r][c], b = sd[l][r0 + r][c + 1], d = sd[l][r0 + r][c + 2];
-            rmx[r] = fmax(fmax(a, b), d);
-            rmn[r] = fmin(fmin(a, b), d);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            nmx[k] = fmax(fmax(rmx[k], rmx[k + 1]), rmx[k + 2]);
-            nmn[k] = fmin(fmin(rmn[k], rmn[k + 1]), rmn[k + 2]);
-        }
-        if (l >= 2) {
-            const int z = l - 1;  // centre layer of the p, q, n window
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int y = cy0 + r0 + k;
-                const double v = sd[z][r0 + k + 1][c + 1];
-                bool cand = false;
-                if (x < W - 1 && y < H - 1 && fabs(v) > dthr) {
-                    const double mx = fmax(fmax(pmx[k], qmx[k]), nmx[k]);
-                    const double mn = fmin(fmin(pmn[k], qmn[k]), nmn[k]);
-                    cand = (v == mx) || (v == mn);
-                }
-                const unsigned long long m = __ballot(cand);
-                if (m) {
-                    unsigned base = 0;
-                    if (lane == 0) base = atomicAdd(counter, (unsigned)__popcll(m));
-                    base = __shfl(base, 0);
-                    const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-                    if (cand && idx < cap) out[idx] = sift_extremum{x, y, z, otag};
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            pmx[k] = qmx[k];
-            pmn[k] = qmn[k];
-            qmx[k] = nmx[k];
-            qmn[k] = nmn[k];
-        }
-    }
-    snapshot_if_last(snap, counter);
-}
-
 // ---------------------------------------------------------------------------
 // k_extrema_stream<NL>: the same test (sift.cpp:227-291, window_size 3) as a
 // streaming scan. One wavefront per task = (octave, strip of 62 centre
@@ -864,8 +757,9 @@ __global__ __launch_bounds__(256) void k_extrema_tiles(const PyrTable* __restric
 // "no neighbour greater" == (v == max)). No LDS, no barrier until the end;
 // 48 B read per pixel and (62 + 2) / 62 x (kExtSeg + 2) / kExtSeg reuse.
 // Candidates: ballot per (row, layer) into a per-wave LDS buffer, one
-// counter atomic per wave. The last workgroup takes the lane snapshot as
-// k_extrema_tiles does.
+// counter atomic per wave. The last workgroup takes the lane snapshot
+// (snapshot_if_last). (A tiled variant staging 66x18 DoG halo tiles in LDS
+// was replaced by this scan in round 2 and removed in round 4.)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double dpp_from_left(double v) {  // lane i <- lane i-1
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
@@ -1198,67 +1092,13 @@ __global__ __launch_bounds__(NT) void k_refine(const PyrTable* __restrict__ pt, 
 }
 
 // ---------------------------------------------------------------------------
-// k_orient: compute_orientations (sift.cpp:447-533), one record per
-// orientation peak; k_descriptor: compute_descriptors + update_histogram +
-// convert_hist_to_desc (sift.cpp:541-682) of every record. Both take one
-// 256-thread workgroup per keypoint from a work counter (persistent grid:
-// dynamic balance over windows of very different sizes). Describing every
+// Orientation: compute_orientations (sift.cpp:447-533), one record per
+// orientation peak (the descriptors are in sift_desc.hip). Describing every
 // oriented keypoint before clean_keypoints (sift.cpp:762, host) gives the
 // same final records: std::unique only drops records equal in (x, y, size,
 // pori), and the kept one is described from its own fields. (One fused
 // orientation+descriptor kernel was measured slower: 242 VGPRs, 2 waves/SIMD.)
-//
-// Orientation
-//  * The (2r+1)^2 window is swept 256 samples at a time (lanes along x, so
-//    the four gradient loads coalesce); wave w takes chunks w, w+4, ...
-//  * Each wave adds weight*magnitude into its own four lane-interleaved
-//    replicas of the histogram (ds_add_f64); the 16 partial histograms are
-//    summed in a fixed order, so results are reproducible run to run. The
-//    per-bin summation order differs from the reference's scan order: the
-//    bins move by a few ulps, the same order of effect as ocml's atan2/exp
-//    against glibc's, far below what a peak decision resolves.
-//  * The in-place circular smoothing (sift.cpp:496-504) is a Gauss-Seidel
-//    recurrence and runs on one lane; peaks are tested one bin per lane.
-// Descriptor
-//  * Accepted samples are enumerated, not searched: for a fixed row, the
-//    reference's test (sift.cpp:651-656) is a conjunction of conditions that
-//    are each monotone in col (col*sin, col*cos, the division and the +1.5
-//    are monotone in IEEE arithmetic), so the accepted columns form one
-//    interval. Each lane estimates the interval of one row analytically and
-//    snaps both ends with the exact test; a wave scan of the lengths then maps
-//    64 consecutive accepted samples to (row, col) per step, so every lane
-//    always works on an accepted sample.
-//  * Rows are dealt round-robin to the four waves; each wave adds into its
-//    own four lane-interleaved replicas of the 4x4x8 f64 histogram, summed in
-//    a fixed order at the end.
-//  * Sample math (default, MODE 1) is f32 once a sample is accepted: the
-//    acceptance test above stays exact f64, and everything after it (rotated
-//    bin position, gradient magnitude, atan2, Gaussian weight, trilinear
-//    split) is continuous in its inputs, so f32 moves a normalised descriptor
-//    float by ~1e-7 (contract 1e-4) and a u8 byte only at a floor boundary.
-//    On MI355X: 70.7 -> 59.4 us per keypoint batch alone, 0.692 -> 0.620 ms
-//    per pipelined 1080p image (profiles/r02_desc). f32 histograms (MODE 2,
-//    ds_add_f32 into 16 replicas per wave) measured slower: 110 us.
-//  * /hist_width is a correctly rounded division by a per-keypoint constant
-//    (div_sum_w with inv = 1/hist_width), the fmods of sift.cpp:667 reduce
-//    exactly to compare-and-subtract (|angle| < 2*2pi, fmod is exact).
-//  * The two normalisation sums (sift.cpp:583-596) are fixed-order wave
-//    reductions (the bins themselves are already summed out of the
-//    reference's order, so a sequential sum would buy no exactness).
 // ---------------------------------------------------------------------------
-constexpr int kOriReps = 4;
-// k_orient: the replicas (4 * kOriReps * (num_bins + 2) doubles) and the
-// Gaussian weight table (kOriTab doubles) live in dynamic LDS sized per
-// launch (17 KB at 36 bins), so orientation workgroups leave room on a CU for
-// other jobs' blur tiles
-constexpr int kOriTab = 1024;
-struct KpLds {
-    double hs[kMaxBins];   // smoothed orientation histogram
-    double pk[kMaxBins];   // orientations of the peaks
-    double red[4];         // normalisation partial sums
-    unsigned k, npk, rec;
-};
-
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const unsigned long long u = __double_as_longlong(v);
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
@@ -1266,225 +1106,28 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
-__global__ __launch_bounds__(256, 4) void k_orient(
-    const PyrTable* __restrict__ pt, DevParams P, const RawKp* __restrict__ raw,
-    const unsigned* __restrict__ raw_begin, const unsigned* __restrict__ n_raw, unsigned cap_raw,
-    sift_kp* __restrict__ recs, RecSide* __restrict__ rec_side, unsigned* __restrict__ n_rec,
-    unsigned cap_rec, unsigned* __restrict__ work) {
-    __shared__ KpLds S;
-    extern __shared__ double ori_dyn[];  // replicas, then the weight table
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const unsigned n = min(*n_raw, cap_raw);
-    const unsigned k0 = min(*raw_begin, n);
-    const int nb = P.num_bins;
-    const int stride = nb + 2;  // pad rotates LDS banks between replicas
-    double* const hist = ori_dyn;
-    double* rep = &hist[(wv * kOriReps + (lane & (kOriReps - 1))) * stride];
-    // Gaussian weights exp(-(i*i + j*j) / denom) depend on k = i*i + j*j
-    // only: a per-keypoint table of the same ocml exp of the same argument
-    // (bit-identical to evaluating it per sample) behind the replicas
-    const int tab_off = 4 * kOriReps * stride;
-    double* wtab = &hist[tab_off];
-    // f32 atan2 picks the bin; within bin_guard of a rounding boundary of
-    // nb*(angle+pi)/2pi the f64 atan2 decides. Error bound of the f32 path:
-    // (float)dx/dy 2^-24 relative, atan2f <= 2 ulp, f32 arithmetic on t <= nb
-    // 3 ulp: below nb * 3e-7, so a 10x guard makes the index exact.
-    const double bin_guard = nb * 3e-6;
-    const float nbf = (float)nb;
-    for (;;) {
-        if (tid == 0) {
-            S.k = k0 + atomicAdd(work, 1u);
-            S.npk = 0;
-        }
-        __syncthreads();
-        const unsigned k = S.k;
-        if (k >= n) break;
-        const RawKp kp = raw[k];
-        const int o = kp.octave;
-        const double inv = 1.0 / pow2i(o);
-        const int x = (int)round(kp.x * inv);
-        const int y = (int)round(kp.y * inv);
-        const double size = kp.size * inv;
-        const double scale = P.ori_sigma_factor * size;
-        const int radius = (int)round(3.0 * scale);
-        const double denom = 2.0 * scale * scale;
-        gdouble* img = gbl(plane(pt, kp.img, o, kp.layer));
-        const int W = pt->w[o], H = pt->h[o];
-        const int side = 2 * radius + 1;
-        const int kmax = 2 * radius * radius;
-        const bool use_tab = kmax < kOriTab;
-        for (int i = tid; i < 4 * kOriReps * stride; i += 256) hist[i] = 0.0;
-        if (use_tab)
-            for (int q = tid; q <= kmax; q += 256) wtab[q] = exp(-q / denom);
-        __syncthreads();
-        // the side x side window flattened over the 256 threads (sample s at
-        // offset (i, j) = (s % side, s / side) - radius); the four gradient
-        // loads of a thread's next sample are issued before the current one
-        // is processed
-        const int nsamp = side * side;
-        // thread's sample s = tid + 256 m at (i, j): advance by 256 samples
-        const int dj = 256 / side, di = 256 - dj * side;
-        int ci_ = tid % side - radius, cj_ = tid / side - radius;
-        auto advance = [&](int& i, int& j) {
-            i += di;
-            j += dj;
-            if (i > radius) {
-                i -= side;
-                ++j;
-            }
-        };
-        // unconditional loads (samples outside the image read pixel (1, 1)),
-        // so the next sample's loads stay in flight while this one is
-        // processed (see describe's fetch)
-        auto fetch = [&](int s, int i, int j, double* v) -> bool {
-            const bool ok =
-                !(s >= nsamp || x + i - 1 < 0 || x + i + 1 >= W || y + j - 1 < 0 || y + j + 1 >= H);
-            const size_t r0 = ok ? (size_t)(y + j) * W + x + i : (size_t)W + 1;
-            v[0] = img[r0 + 1];
-            v[1] = img[r0 - 1];
-            v[2] = img[r0 - W];
-            v[3] = img[r0 + W];
-            return ok;
-        };
-        double cv[4], nv[4];
-        bool cok = fetch(tid, ci_, cj_, cv);
-        int ni_ = ci_, nj_ = cj_;
-        advance(ni_, nj_);
-        for (int s = tid; s < nsamp; s += 256) {
-            const bool nok = fetch(s + 256, ni_, nj_, nv);
-            if (cok) {
-                const double dx = cv[0] - cv[1];
-                const double dy = cv[2] - cv[3];
-                const double mag = sqrt(dx * dx + dy * dy);
-                const int k2 = ci_ * ci_ + cj_ * cj_;
-                const double wgt = use_tab ? wtab[k2] : exp(-k2 / denom);
-                const float t = nbf * (atan2f((float)dy, (float)dx) + (float)kPi) *
-                                (float)(1.0 / kTwoPi);
-                int hidx = (int)rintf(t);
-                const bool tiny = (dx != 0.0 && fabs(dx) < 1e-30) || (dy != 0.0 && fabs(dy) < 1e-30);
-                if (fabs((double)t - floor((double)t) - 0.5) < bin_guard || tiny)
-                    hidx = (int)round(nb * (atan2(dy, dx) + kPi) / kTwoPi);  // exact path
-                hidx = (hidx < nb) ? hidx : 0;
-                atomicAdd(&rep[hidx], wgt * mag);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
-            cok = nok;
-            ci_ = ni_;
-            cj_ = nj_;
-            advance(ni_, nj_);
-        }
-        __syncthreads();
-        if (nb <= 64) {
-            // smoothing (sift.cpp:496-504) on wave 0 in registers: lane b
-            // holds bin b; the Gauss-Seidel chain runs through wave-uniform
-            // values, one dependent fma+add per bin
-            if (wv == 0) {
-                double h = 0.0;
-                if (lane < nb)
-                    for (int r = 0; r < 4 * kOriReps; ++r) h += hist[r * stride + lane];
-                for (int it = 0; it < kSmoothIters; ++it) {
-                    const double hn = __shfl(h, lane + 1 < nb ? lane + 1 : 0);  // old h[i+1]
-                    const double c = 0.5 * h, d = 0.25 * hn;
-                    double prev = readlane_f64(h, nb - 1);  // h[i-1] for i = 0: old
-                    double first_new = 0.0, mine = h;
-                    for (int i = 0; i < nb; ++i) {
-                        const double ci = readlane_f64(c, i);
-                        // h[i+1]: old, except for i = nb-1 > 0 where it is
-                        // the already-updated h[0]
-                        const double di = (i + 1 == nb && i > 0) ? 0.25 * first_new
-                                                                  : readlane_f64(d, i);
-                        // (0.25 prev + 0.5 h1) + 0.25 h2: 0.25 * prev is exact
-                        // (bins >= 0, never subnormal), so the fma rounds the
-                        // same sum once
-                        const double v = fma(0.25, prev, ci) + di;
-                        if (lane == i) mine = v;
-                        prev = v;
-                        if (i == 0) first_new = v;
-                    }
-                    h = mine;
-                }
-                if (lane < nb) S.hs[lane] = h;
-            }
-        } else {
-            for (int b = tid; b < nb; b += 256) {
-                double v = 0.0;
-                for (int r = 0; r < 4 * kOriReps; ++r) v += hist[r * stride + b];
-                S.hs[b] = v;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                for (int it = 0; it < kSmoothIters; ++it) {
-                    double prev = S.hs[nb - 1];  // h[i-1] for i = 0: not yet updated
-                    const double h0_old = S.hs[0];
-                    double first_new = 0.0;
-                    for (int i = 0; i < nb; ++i) {
-                        const double h1 = S.hs[i];
-                        const double h2 =
-                            (i + 1 < nb) ? S.hs[i + 1] : (i == 0 ? h0_old : first_new);
-                        const double v = fma(0.25, prev, 0.5 * h1) + 0.25 * h2;
-                        S.hs[i] = v;
-                        prev = v;
-                        if (i == 0) first_new = v;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        // max over bins (histogram entries are >= 0): every wave reduces all
-        double mx = 0.0;
-        for (int b = lane; b < nb; b += 64) mx = fmax(mx, S.hs[b]);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
-        for (int i = tid; i < nb; i += 256) {
-            const double h0 = S.hs[i == 0 ? nb - 1 : i - 1];
-            const double h1 = S.hs[i];
-            const double h2 = S.hs[i + 1 == nb ? 0 : i + 1];
-            if (h1 > h0 && h1 > h2 && h1 > (P.peak_ratio * mx)) {
-                double fi = i + 0.5 * (h0 - h2) / (h0 - 2 * h1 + h2);
-                fi = fmod(fi + nb, (double)nb);
-                double ori = kTwoPi * fi / nb;
-                ori = fmod(ori + kTwoPi, kTwoPi);
-                S.pk[atomicAdd(&S.npk, 1u)] = ori;
-            }
-        }
-        __syncthreads();
-        const unsigned npk = S.npk;
-        double rx = kp.x, ry = kp.y, rs = kp.size;
-        if (P.double_image) {  // sift.cpp:522-526
-            rx /= 2;
-            ry /= 2;
-            rs /= 2;
-        }
-        for (unsigned p = tid; p < npk; p += 256) {
-            const unsigned rec = atomicAdd(n_rec, 1u);
-            if (rec < cap_rec) {
-                sift_kp& r = recs[rec];
-                r.x = rx;
-                r.y = ry;
-                r.octave = kp.octave;
-                r.layer = kp.layer;
-                r.size = rs;
-                r.pori = S.pk[p];
-                rec_side[rec] = RecSide{kp.off0, kp.img, 0};
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // ---------------------------------------------------------------------------
-// k_orient_wave (the default): compute_orientations (sift.cpp:447-533) with
-// one WAVEFRONT per refined keypoint, four independent waves per workgroup
-// pulling keypoints from the work counter; no workgroup barrier. Same
-// arithmetic as k_orient (f32 bin with the guarded exact f64 path, Gaussian
-// weights from a per-keypoint table of the same ocml exp, f64 replicas
-// summed in a fixed order, Gauss-Seidel smoothing in registers), but the
-// per-keypoint setup, table, smoothing and peak search run once per keypoint
-// instead of once per wave of a 256-thread workgroup. Per-wave dynamic LDS:
-// 16 replica-interleaved copies of the histogram, the weight table
-// (kOriWTab doubles), and for num_bins > 64 the smoothed histogram.
+// k_orient_wave: compute_orientations (sift.cpp:447-533) with one WAVEFRONT
+// per refined keypoint, four independent waves per workgroup pulling
+// keypoints from the work counter; no workgroup barrier.
+//  * The (2r+1)^2 window is swept 64 samples at a time (lanes along x, so
+//    the four gradient loads coalesce).
+//  * The bin of a sample comes from an f32 atan2f; whenever it lies within
+//    nb * 3e-6 of a rounding boundary (10x the f32 path's error bound) or
+//    |dx|, |dy| is tiny, the f64 atan2 decides, so the bin index equals the
+//    f64 one. Gaussian weights come from a per-keypoint table of the same
+//    ocml exp of the same argument (bit-identical to evaluating per sample).
+//  * weight * magnitude goes into lane-interleaved f64 replicas of the
+//    histogram (ds_add_f64), summed in a fixed order: reproducible run to
+//    run. The per-bin summation order differs from the reference's scan
+//    order: the bins move by a few ulps, the same order of effect as ocml's
+//    atan2/exp against glibc's, far below what a peak decision resolves.
+//  * The in-place circular smoothing (sift.cpp:496-504) is a Gauss-Seidel
+//    recurrence, run in registers (lane = bin); peaks are tested one bin per
+//    lane. (A 256-thread-workgroup-per-keypoint variant repeated the setup,
+//    table, smoothing and peak search in every wave; removed in round 4.)
+// Per-wave dynamic LDS: the histogram replicas, the weight table (kOriWTab
+// doubles), and for num_bins > 64 the smoothed histogram.
 // ---------------------------------------------------------------------------
 #ifndef SIFT_ORIW_TAB
 #define SIFT_ORIW_TAB 512
@@ -1520,7 +1163,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
     double* const rep = hist + (lane & (kOriWReps - 1));  // bin b at rep[b * kOriWReps]
     double* const wtab = hist + kOriWReps * nb;
     double* const hs = wtab + kOriWTab;  // num_bins > 64 only
-    const double bin_guard = nb * 3e-6;  // see k_orient
+    const double bin_guard = nb * 3e-6;  // f32 bin error bound x 10 (see above)
     const float nbf = (float)nb;
     for (;;) {
         unsigned claim = 0;
@@ -1629,7 +1272,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
         };
         if (nb <= 64) {
             // lane b holds bin b; the Gauss-Seidel chain runs through
-            // wave-uniform values, one dependent fma+add per bin (k_orient)
+            // wave-uniform values, one dependent fma+add per bin
             double h = 0.0;
             if (lane < nb)  // fixed order per bin, rotated by lane (banks)
 #pragma unroll
@@ -1748,21 +1391,9 @@ static_assert(kMaxTemplR == 16, "blur tables must cover 1..kMaxTemplR");
 // strips: the small levels are latency-bound).
 BlurShape blur_shape_for(int W, int H, int R) {
     const size_t px = (size_t)W * H;
-    // SIFT_BLUR_ROWS: strip rows on octave-0-sized levels (A/B sweeps)
-    static const int big_rows = [] {
-        const char* e = std::getenv("SIFT_BLUR_ROWS");
-        const int v = e ? std::atoi(e) : 0;
-        return v >= 8 && v <= 512 ? v : 32;
-    }();
-    // SIFT_BLUR_COLS=1: one column per lane on octave-0-sized levels (A/B)
-    static const int big_cols = [] {
-        const char* e = std::getenv("SIFT_BLUR_COLS");
-        return e && std::atoi(e) == 1 ? 1 : 2;
-    }();
     BlurShape b;
     b.cols = (!(W & 1) && px >= ((size_t)1 << 20)) ? 2 : 1;
-    if (px >= ((size_t)4 << 20) && big_cols == 1) b.cols = 1;
-    b.rows = px >= ((size_t)4 << 20) ? big_rows : 16;
+    b.rows = px >= ((size_t)4 << 20) ? 32 : 16;  // 48 / 64 / 96 rows measured slower
     if (R > 12 && b.cols == 2) b.rows = 16;
     if (b.rows > H) b.rows = H;
     return b;
@@ -2021,34 +1652,6 @@ hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, i
     return hipGetLastError();
 }
 
-hipError_t launch_extrema_tiles(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
-                                int n_gauss, int thr, sift_extremum* out, unsigned* counter,
-                                unsigned cap, unsigned* snap, hipStream_t s) {
-    const int blocks = eg.first_tile[eg.n];
-    if (blocks == 0 || n_img == 0)  // nothing to scan: the snapshot is the live counters
-        return snap ? launch_snapshot(counter, snap, s, 0, 3) : hipSuccess;
-    const dim3 grid(blocks, n_img);
-    switch (n_gauss) {
-#define SIFT_EXT_CASE(NL)                                                                  \
-    case NL:                                                                               \
-        hipLaunchKernelGGL((k_extrema_tiles<NL>), grid, dim3(256), 0, s, d_pt, eg, thr, out, \
-                           counter, cap, snap);                                            \
-        return hipGetLastError();
-        SIFT_EXT_CASE(4)
-        SIFT_EXT_CASE(5)
-        SIFT_EXT_CASE(6)
-        SIFT_EXT_CASE(7)
-        SIFT_EXT_CASE(8)
-        SIFT_EXT_CASE(9)
-        SIFT_EXT_CASE(10)
-        SIFT_EXT_CASE(11)
-        SIFT_EXT_CASE(12)
-#undef SIFT_EXT_CASE
-        default:
-            return hipErrorInvalidValue;
-    }
-}
-
 hipError_t launch_extrema_stream(const PyrTable* d_pt, const ExtremaGrid& eg, int n_img,
                                  int n_gauss, int thr, sift_extremum* out, unsigned* counter,
                                  unsigned cap, unsigned* snap, hipStream_t s, hipEvent_t e0,
@@ -2094,49 +1697,25 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
                          RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s,
                          hipEvent_t e0, hipEvent_t e1) {
-    // SIFT_REFINE_NT (64 or 256 threads per workgroup), SIFT_REFINE_WGS: A/B knobs
-    static const int nt = [] {
-        const char* e = std::getenv("SIFT_REFINE_NT");
-        return (e && std::atoi(e) == 256) ? 256 : 64;
-    }();
-    static const int cpw = [] {  // SIFT_REFINE_CPW: candidates per wavefront (64, 32, 16)
-        const char* e = std::getenv("SIFT_REFINE_CPW");
-        const int v = e ? std::atoi(e) : 64;
-        return v == 16 ? 16 : v == 32 ? 32 : 64;
-    }();
-    static const unsigned max_blocks = [] {
-        const char* e = std::getenv("SIFT_REFINE_WGS");
-        return e ? (unsigned)std::max(1, std::atoi(e)) : 262144u / nt;
-    }();
-    const unsigned per_wg = (unsigned)(nt / 64 * cpw);
-    unsigned blocks = (cap_cand + per_wg - 1) / per_wg;
-    if (blocks > max_blocks) blocks = max_blocks;
-    if (blocks == 0) blocks = 1;
-#define SIFT_REFINE_LAUNCH(NT_, CPW_)                                                           \
-    launch_timed(k_refine<NT_, CPW_>, dim3(blocks), dim3(NT_), 0, s, e0, e1, d_pt, P, cand,    \
-                 cand_begin, n_cand, cap_cand, out, n_out, cap_out)
-    if (nt == 256) return SIFT_REFINE_LAUNCH(256, 64);
-    if (cpw == 16) return SIFT_REFINE_LAUNCH(64, 16);
-    if (cpw == 32) return SIFT_REFINE_LAUNCH(64, 32);
-    return SIFT_REFINE_LAUNCH(64, 64);
-#undef SIFT_REFINE_LAUNCH
+    // one wavefront per workgroup, a candidate per lane: a batch's few
+    // thousand candidates spread over ~100 CUs (256-thread workgroups, 16 or
+    // 32 candidates per wave measured slower)
+    constexpr unsigned kPerWg = 64;
+    unsigned blocks = (cap_cand + kPerWg - 1) / kPerWg;
+    blocks = std::max(1u, std::min(blocks, 262144u / kPerWg));
+    return launch_timed(k_refine<64, 64>, dim3(blocks), dim3(64), 0, s, e0, e1, d_pt, P, cand,
+                        cand_begin, n_cand, cap_cand, out, n_out, cap_out);
 }
 
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
-                         unsigned* work, unsigned wgs, int mode, hipStream_t s,
-                         hipEvent_t e0, hipEvent_t e1) {
-    unsigned blocks = wgs;  // persistent: workgroups pull keypoints
-    if (mode == 1) {  // four waves per workgroup, a keypoint per wave
-        blocks = std::min<unsigned>(blocks, cap_raw > 0 ? (cap_raw + 3) / 4 : 1);
-        const size_t lds = (size_t)4 * ori_wave_lds_doubles(P.num_bins) * sizeof(double);
-        return launch_timed(k_orient_wave, dim3(blocks), dim3(256), lds, s, e0, e1, d_pt, P, raw,
-                            raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work);
-    }
-    if (blocks > cap_raw) blocks = cap_raw > 0 ? cap_raw : 1;
-    const size_t lds = (size_t)(4 * kOriReps * (P.num_bins + 2) + kOriTab) * sizeof(double);
-    return launch_timed(k_orient, dim3(blocks), dim3(256), lds, s, e0, e1, d_pt, P, raw,
+                         unsigned* work, unsigned wgs, hipStream_t s, hipEvent_t e0,
+                         hipEvent_t e1) {
+    // persistent: four waves per workgroup, a keypoint per wave
+    const unsigned blocks = std::min<unsigned>(wgs, cap_raw > 0 ? (cap_raw + 3) / 4 : 1);
+    const size_t lds = (size_t)4 * ori_wave_lds_doubles(P.num_bins) * sizeof(double);
+    return launch_timed(k_orient_wave, dim3(blocks), dim3(256), lds, s, e0, e1, d_pt, P, raw,
                         raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work);
 }
 
