@@ -488,9 +488,13 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
         if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 3));
     }
     const unsigned* b = begin ? begin : zeros;
-    // persistent grid of this chain: kp_wgs / desc_wgs per image
-    const unsigned ori_wgs = std::min(kKpWgsMax, ctx->kp_wgs * (unsigned)n_img);
-    const unsigned desc_wgs = std::min(kKpWgsMax, ctx->desc_wgs * (unsigned)n_img);
+    // persistent grid of this chain: kp_wgs / desc_wgs per image. The last
+    // chain of a job alone on the chip (two keypoint lanes) runs after its
+    // whole pyramid, with no blur left to starve: it takes kKpWgsMax
+    const bool tail = s.lanes > 1 && o_end == g.octaves;
+    const unsigned ori_wgs = tail ? kKpWgsMax : std::min(kKpWgsMax, ctx->kp_wgs * (unsigned)n_img);
+    const unsigned desc_wgs =
+        tail ? kKpWgsMax : std::min(kKpWgsMax, ctx->desc_wgs * (unsigned)n_img);
     hipEvent_t r0, r1, q0, q1, d0, d1;  // profiling events of the keypoint stages
     if (prof_events(ctx, s, &r0, &r1, 0.0, SIFT_PROF_REFINE) != SIFT_OK ||
         prof_events(ctx, s, &q0, &q1, 0.0, SIFT_PROF_ORIENT) != SIFT_OK ||

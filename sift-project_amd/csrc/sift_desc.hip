@@ -1,11 +1,15 @@
 // sift_desc.hip — compute_descriptors + update_histogram +
 // convert_hist_to_desc (reference src/sift.cpp:541-682) on gfx950.
 //
-// Default (desc_mode 0): k_descriptor_split<true>, every per-sample
-// operation in f64 as the reference does it (sift.cpp:641-678), one record
-// per 256-thread workgroup, its rows dealt to the four waves.
-// desc_mode 1 / 2 keep the round-3 kernels with f32 sample math for A/B
-// (k_descriptor_wave: one wave per record; k_descriptor_split<false>).
+// Two kernel shapes share one sample walk (desc_walk) and two sample bodies:
+//  * k_descriptor_split<F64>: one record per 256-thread workgroup, the
+//    window's rows dealt to its four waves (default: desc_mode 0, F64);
+//  * k_descriptor_wave<F64>: one record per wavefront, four independent
+//    waves per workgroup (A/B: desc_mode 1 = f32 sample math, round 3's
+//    default; desc_mode 3 = f64 sample math);
+// desc_mode 2 = the split kernel with f32 sample math (A/B).
+// F64 is the reference's arithmetic: every per-sample operation in double
+// (sift.cpp:641-678); f32 sample math moves the normalised floats by ~1e-7.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -15,19 +19,25 @@
 #include "sift_math64.h"
 
 // replicas of the 4x4x8 f64 histogram per wave (power of two <= 16) and the
-// minimum workgroups per CU of k_descriptor_split
+// minimum workgroups per CU, per kernel shape
 #ifndef SIFT_DSPLIT_REPS
 #define SIFT_DSPLIT_REPS 16
 #endif
 #ifndef SIFT_DSPLIT_OCC
 #define SIFT_DSPLIT_OCC (SIFT_DSPLIT_REPS >= 16 ? 2 : 4)
 #endif
+#ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
+#define SIFT_DESCW_REPS 16
+#endif
+#ifndef SIFT_DESCW_OCC
+#define SIFT_DESCW_OCC (SIFT_DESCW_REPS >= 16 ? 2 : 5)
+#endif
 
 namespace sift_amd {
 
 namespace {
 
-// atan2 in f32 for the descriptor's sample math: octant reduction to
+// atan2 in f32 for the f32 sample math: octant reduction to
 // a = min(|x|, |y|) / max(|x|, |y|) (v_rcp_f32, 1 ulp), atan(a) as
 // a + a^3 p(a^2) with a degree-7 p fitted for minimum max error on [0, 1]
 // (8.5e-8 rad in f32 arithmetic over 2e6 points), then the quadrant fix-up.
@@ -53,331 +63,331 @@ __device__ __forceinline__ float atan2_f32(float y, float x) {
     return copysignf(th, y);
 }
 
-
-// ---------------------------------------------------------------------------
-// k_descriptor_wave (desc_mode 1, the default): one WAVEFRONT per record
-// (sift.cpp:610-682), four independent waves per workgroup pulling records
-// from the work counter; no workgroup barrier anywhere.
-//
-// Per-record cost was dominated by work every wave of the 256-thread
-// version repeated (record setup with f64 sin/cos, the f64 row-interval
-// solve with exact snapping, histogram zero/reduce/normalise): ~1150 VALU
-// instructions per wave per record against ~1100 for the samples
-// themselves (r02 SQ counters). Here a record's setup runs once, and:
-//  * The sample set is enumerated as an f32 SUPERSET of the reference's
-//    rotated box (row intervals widened by 0.01 column). No exact test is
-//    needed: a sample's trilinear weights vanish continuously at the box
-//    edges (row_bin -> -1 puts weight fr -> 0 on row 0 and the rest on the
-//    skipped row -1; row_bin -> 4 puts 1 - fr -> 0 on row 3), so a sample
-//    just outside contributes exactly nothing (its cells are skipped) and
-//    one just inside contributes ~1e-7 of its magnitude — the same order as
-//    the f32 sample math itself (contract: 1e-4 on the floats).
-//  * Sample math as describe<1> (f32, f64 histograms); the integer bounds
-//    (radius, image border) are exact.
-//  * kDescWReps replica-interleaved f64 copies of the 4x4x8 histogram per
-//    wave; the 128 bins are reduced two per lane (bins l and l + 64), the
-//    two normalisation sums are in-wave reductions.
-// A wave's LDS instructions execute in order, so zeroing -> accumulation
-// -> reduction -> next record's zeroing needs only compiler ordering
-// (wave_sync).
-// ---------------------------------------------------------------------------
-#ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
-#define SIFT_DESCW_REPS 16
-#endif
-#ifndef SIFT_DESCW_OCC  // min workgroups per CU (16 replicas: 64 KB LDS each)
-#define SIFT_DESCW_OCC (SIFT_DESCW_REPS >= 16 ? 2 : 5)
-#endif
-#ifndef SIFT_DESCW_WALK
-#define SIFT_DESCW_WALK 0
-#endif
-#ifndef SIFT_DESCW_AHEAD
-#define SIFT_DESCW_AHEAD 1
-#endif
-constexpr int kDescWReps = SIFT_DESCW_REPS;
-static_assert(kDescWReps >= 1 && kDescWReps <= 16 && (kDescWReps & (kDescWReps - 1)) == 0,
-              "replicas: a power of two <= 16");
-// Replica-interleaved layout: bin i of replica r at hist[i * kDescWReps + r],
-// r = lane % kDescWReps. ds_add_f64 serves 16 lanes per LDS cycle over 32
-// banks (bank = dword address mod 32); a lane's bank pair is then
-// 2 (i * kDescWReps + r) mod 32, so with 16 replicas every lane of a group
-// owns its bank pair whatever bins the samples hit (conflict-free), with 8
-// two lanes share a replica and collide only on bins of equal parity. (A
-// replica-major layout, r * stride + i, leaves the bank to the bin: the
-// atomics measured ~1 extra LDS cycle per LDS cycle, lane % 4 or % 16 alike.)
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
     return v;
 }
 
-__global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
-    const PyrTable* __restrict__ pt, DevParams P, sift_kp* __restrict__ recs,
-    const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
-    const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
-    unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kDescWReps];
-    set_job_prio(pt->jp, 0);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double* const hist = hist_all + wv * 128 * kDescWReps;
-    double* const rep = hist + (lane & (kDescWReps - 1));  // bin i at rep[i * kDescWReps]
-    const unsigned n = min(*n_rec, cap_rec);
-    const unsigned k0 = min(*rec_begin, n);
-    // the launch's record range is fixed before it starts (orientation has
-    // completed); the host reads it after the chain's completion event
-    if (ex.cnt && blockIdx.x == 0 && threadIdx.x == 0) {
-        ex.cnt[0] = k0;
-        ex.cnt[1] = n;
+// ---------------------------------------------------------------------------
+// Per-record geometry (sift.cpp:616-639), wave-uniform.
+// ---------------------------------------------------------------------------
+struct DescRecord {
+    double kx, ky, ksize, pori;
+    int o, layer;
+    RecSide side;
+    const double* img;
+    int W, H, x, y, radius;
+    double hw, ihw, sa, ca;      // hist_width, 1 / hist_width, sin / cos (F64)
+    float saf, caf, ihwf, porif, limf;
+};
+
+// sa / ca: the f64 sin / cos of pori when the caller already has them
+// (F64, split kernel: computed once per record); otherwise computed here
+template <bool F64>
+__device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevParams& P,
+                                                  const sift_kp& R, const RecSide& side,
+                                                  const double2* sc) {
+    DescRecord d;
+    d.kx = R.x;
+    d.ky = R.y;
+    d.ksize = R.size;
+    d.pori = R.pori;
+    d.o = R.octave;
+    d.layer = R.layer;
+    d.side = side;
+    d.img = plane(pt, side.img, d.o, d.layer);
+    d.W = pt->w[d.o];
+    d.H = pt->h[d.o];
+    const double inv = P.double_image ? (1.0 / pow2i(d.o - 1)) : (1.0 / pow2i(d.o));
+    d.x = (int)(d.kx * inv);  // truncation (sift.cpp:620-624)
+    d.y = (int)(d.ky * inv);
+    d.hw = P.desc_scale_factor * (d.ksize * inv);
+    const double rr = round(d.hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
+    const double diag = sqrt((double)(d.W * d.W + d.H * d.H));
+    d.radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
+    d.ihw = 1.0 / d.hw;
+    d.sa = 0.0;
+    d.ca = 1.0;
+    if (F64) {
+        if (sc) {
+            d.sa = sc->x;
+            d.ca = sc->y;
+        } else {
+            d.sa = sin(d.pori);
+            d.ca = cos(d.pori);
+        }
+        d.saf = (float)d.sa;
+        d.caf = (float)d.ca;
+    } else {
+        sincosf((float)d.pori, &d.saf, &d.caf);
     }
-    constexpr float kHalfW = (float)(kDescW / 2 - 0.5);  // row_bin = row_rot + 1.5
+    d.ihwf = (float)d.ihw;
+    d.porif = (float)d.pori;
+    d.limf = (float)((0.5 * kDescW + 0.5) * d.hw);  // |row_rot|, |col_rot| < 2.5 hw
+    return d;
+}
+
+// ---------------------------------------------------------------------------
+// One sample (col, row) with gradient loads cv = I(x+1), I(x-1), I(y-1),
+// I(y+1) into this lane's replica `rep` (bin i at rep[i * NR]).
+// F64: the reference's expressions (sift.cpp:641-678): row_rot / col_rot
+// with the correctly rounded division by hist_width, (row_rot + 2) - 0.5,
+// sqrt, atan2 - pori and the two fmods (exact compare-and-subtract),
+// exp(-(row_rot^2 + col_rot^2) / 8), the trilinear split of
+// update_histogram (sift.cpp:541-571). Samples of the enumerated f32
+// superset outside the box get row_bin / col_bin <= -1 or >= 4 from these
+// exact expressions: their cells are all skipped, or take weight 0
+// (row_bin = -1 exactly), so the contributing sample set is the reference's.
+// ---------------------------------------------------------------------------
+template <int NR>
+__device__ __forceinline__ void add_sample_f64(double* rep, int scol, int srow, const double* cv,
+                                               const DescRecord& d, const double2* atab) {
+    constexpr double kBinsPerRad = kDescBins / kTwoPi;  // sift.cpp:628
+    const double dcol = (double)scol, drow = (double)srow;
+    const double row_rot = div_sum_w(dcol * d.sa + drow * d.ca, d.hw, d.ihw);
+    const double col_rot = div_sum_w(dcol * d.ca - drow * d.sa, d.hw, d.ihw);
+    const double rb = row_rot + kDescW / 2 - 0.5;
+    const double cb = col_rot + kDescW / 2 - 0.5;
+    const double dx = cv[0] - cv[1];
+    const double dy = cv[2] - cv[3];
+    const double mag = sqrt_f64(dx * dx + dy * dy);
+    double ang = atan2_f64(dy, dx, atab) - d.pori;
+    // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi: fmod(a, M) =
+    // a - trunc(a/M) M is exact here, so compare-and-subtract reproduces it
+    if (ang >= kTwoPi) ang -= kTwoPi;
+    else if (ang <= -kTwoPi) ang += kTwoPi;
+    ang += kTwoPi;
+    if (ang >= kTwoPi) ang -= kTwoPi;
+    if (ang >= kTwoPi) ang -= kTwoPi;
+    const double ob = ang * kBinsPerRad;
+    const double wgt = exp_f64(-(row_rot * row_rot + col_rot * col_rot) / (0.5 * kDescW * kDescW));
+    const double m = mag * wgt;
+    const double fbr = floor(rb), fbc = floor(cb), fbo = floor(ob);
+    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
+    const double fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
+#pragma unroll
+    for (int rq = 0; rq <= 1; ++rq) {
+        const int ri = br + rq;
+        if ((unsigned)ri >= (unsigned)kDescW) continue;
+        const double vr = m * ((rq == 0) ? 1.0 - fr : fr);
+#pragma unroll
+        for (int cq = 0; cq <= 1; ++cq) {
+            const int ci = bc + cq;
+            if ((unsigned)ci >= (unsigned)kDescW) continue;
+            const double vc = vr * ((cq == 0) ? 1.0 - fc : fc);
+            double* hb = &rep[(ri * 32 + ci * 8) * NR];
+            atomicAdd(&hb[(bo & 7) * NR], vc * (1.0 - fo));
+            atomicAdd(&hb[((bo + 1) & 7) * NR], vc * fo);
+        }
+    }
+}
+
+// f32 sample math (A/B): rotated bin position, magnitude, atan2, exp2 and
+// the trilinear split in f32, histograms in f64
+template <int NR>
+__device__ __forceinline__ void add_sample_f32(double* rep, int scol, int srow, const double* cv,
+                                               const DescRecord& d) {
+    constexpr float kHalfW = (float)(kDescW / 2 - 0.5);
     const float wscale = (float)(-1.4426950408889634 / (0.5 * kDescW * kDescW));
-    for (;;) {
-        unsigned claim = 0;
-        if (lane == 0) claim = atomicAdd(work, 1u);
-        const unsigned k = k0 + __builtin_amdgcn_readfirstlane(claim);
-        if (k >= n) break;
-        // ---- record setup (wave-uniform)
-        const sift_kp& R = recs[k];
-        const double kx = R.x, ky = R.y, ksize = R.size, pori = R.pori;
-        const int o = R.octave, layer = R.layer;
-        const RecSide rside = rec_side[k];
-        gdouble* img = gbl(plane(pt, rside.img, o, layer));
-        const int W = pt->w[o], H = pt->h[o];
-        const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
-        const int x = (int)(kx * inv);
-        const int y = (int)(ky * inv);
-        const double hw = P.desc_scale_factor * (ksize * inv);
-        const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
-        const double diag = sqrt((double)(W * W + H * H));
-        const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
-        const int side = 2 * radius + 1;
-        float saf, caf;
-        sincosf((float)pori, &saf, &caf);
-        const float ihwf = (float)(1.0 / hw);
-        const float porif = (float)pori;
-        // |row_rot| < 2.5 and |col_rot| < 2.5, in units of hw
-        const float limf = (float)((0.5 * kDescW + 0.5) * hw);
-        for (int i = lane; i < 64 * kDescWReps; i += 64)
-            reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
-        wave_sync();
-        // ---- rows in groups of 64 (lane = row), samples 64 at a time
-        for (int g0 = 0; g0 < side; g0 += 64) {
-            const int row = g0 + lane - radius;
-            int lo = 0, len = 0;
-            if (g0 + lane < side && row + y > 0 && row + y < H - 1) {
-                const float fr = (float)row, ra = fr * caf, rs = fr * saf;
-                float clo = (float)max(-radius, 1 - x), chi = (float)min(radius, W - 2 - x);
-                // |c sa + r ca| < lim and |c ca - r sa| < lim, widened by 0.01
-                // column (f32 rounding of the bounds is far below that)
-                if (fabsf(saf) > 1e-6f) {
-                    const float is = 1.0f / saf;
-                    const float a1 = (-limf - ra) * is, a2 = (limf - ra) * is;
-                    clo = fmaxf(clo, fminf(a1, a2) - 0.01f);
-                    chi = fminf(chi, fmaxf(a1, a2) + 0.01f);
-                } else if (!(fabsf(ra) < limf + 0.01f)) {
-                    chi = clo - 1.0f;
-                }
-                if (fabsf(caf) > 1e-6f) {
-                    const float ic = 1.0f / caf;
-                    const float b1 = (-limf + rs) * ic, b2 = (limf + rs) * ic;
-                    clo = fmaxf(clo, fminf(b1, b2) - 0.01f);
-                    chi = fminf(chi, fmaxf(b1, b2) + 0.01f);
-                } else if (!(fabsf(rs) < limf + 0.01f)) {
-                    chi = clo - 1.0f;
-                }
-                lo = (int)ceilf(clo);
-                const int hi = (int)floorf(chi);
-                len = hi >= lo ? hi - lo + 1 : 0;
-            }
-            int pre = len;  // inclusive scan of the row lengths
+    const float fcol = (float)scol, frow = (float)srow;
+    const float row_rot = fmaf(fcol, d.saf, frow * d.caf) * d.ihwf;
+    const float col_rot = fmaf(fcol, d.caf, -(frow * d.saf)) * d.ihwf;
+    const float rb = row_rot + kHalfW;
+    const float cb = col_rot + kHalfW;
+    const float dx = (float)(cv[0] - cv[1]);
+    const float dy = (float)(cv[2] - cv[3]);
+    const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
+    const float ob = (atan2_f32(dy, dx) - d.porif) * (float)(kDescBins / kTwoPi);
+    const float wgt = __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
+    const float m = mag * wgt;
+    const float fbr = floorf(rb), fbc = floorf(cb), fbo = floorf(ob);
+    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
+    const float fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int t = __shfl_up(pre, off);
-                if (lane >= off) pre += t;
-            }
-            const int total = __builtin_amdgcn_readlane(pre, 63);
-            // (row, col) of sample t0 + lane; false past the end. Its row r
-            // is the number of rows whose inclusive prefix is <= t: a
-            // branch-free binary search over the 64 prefixes (the scalar
-            // walk over the rows a block touches cost ~20 SALU per block)
-#if SIFT_DESCW_WALK
-            int cur = 0;  // A/B: the scalar walk
-#endif
-            auto locate = [&](int t0, int& srow, int& scol) -> bool {
-                const int t = t0 + lane;
-#if SIFT_DESCW_WALK
-                int r = cur, nxt = cur;
-                for (int q = cur; q < 64; ++q) {
-                    const int pq = __builtin_amdgcn_readlane(pre, q);
-                    if (pq > t0 + 63) break;
-                    r += (pq <= t) ? 1 : 0;
-                    nxt = q + 1;
-                }
-                cur = nxt;
-#else
-                int r = 0;
+    for (int rq = 0; rq <= 1; ++rq) {
+        const int ri = br + rq;
+        if ((unsigned)ri >= (unsigned)kDescW) continue;
+        const float vr = m * ((rq == 0) ? 1.0f - fr : fr);
 #pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (__shfl(pre, r + step - 1) <= t) r += step;
-#endif
-                const int lo_r = __shfl(lo, r);
-                const int ex_r = __shfl(pre, r) - __shfl(len, r);
-                srow = g0 + r - radius;
-                scol = lo_r + (t - ex_r);
-                return t < total;
-            };
-            // gradient loads issued unconditionally (see describe's fetch)
-            auto fetch = [&](bool ok, int srow, int scol, double* v) {
-                const size_t r0 = ok ? (size_t)(srow + y) * W + scol + x : (size_t)W + 1;
-                v[0] = img[r0 + 1];
-                v[1] = img[r0 - 1];
-                v[2] = img[r0 - W];
-                v[3] = img[r0 + W];
-            };
-            // kAhead blocks of 64 samples whose gradient loads are in flight
-            // while the current block is processed
-            constexpr int kAhead = SIFT_DESCW_AHEAD;
-            int srow = 0, scol = 0, qrow[kAhead], qcol[kAhead];
-            bool qok[kAhead];
-            double cv[4] = {0.0, 0.0, 0.0, 0.0}, qv[kAhead][4];
-            bool cok = total > 0 && locate(0, srow, scol);
-            fetch(cok, srow, scol, cv);
-#pragma unroll
-            for (int a = 0; a + 1 < kAhead; ++a) {
-                qrow[a] = qcol[a] = 0;
-                qok[a] = 64 * (a + 1) < total && locate(64 * (a + 1), qrow[a], qcol[a]);
-                fetch(qok[a], qrow[a], qcol[a], qv[a]);
-            }
-            for (int t0 = 0; t0 < total; t0 += 64) {
-                {
-                    int& nrow = qrow[kAhead - 1];
-                    int& ncol = qcol[kAhead - 1];
-                    nrow = ncol = 0;
-                    qok[kAhead - 1] =
-                        t0 + 64 * kAhead < total && locate(t0 + 64 * kAhead, nrow, ncol);
-                    fetch(qok[kAhead - 1], nrow, ncol, qv[kAhead - 1]);
-                }
-                if (cok) {
-                    const float fcol = (float)scol, frow = (float)srow;
-                    const float row_rot = fmaf(fcol, saf, frow * caf) * ihwf;
-                    const float col_rot = fmaf(fcol, caf, -(frow * saf)) * ihwf;
-                    const float rb = row_rot + kHalfW;
-                    const float cb = col_rot + kHalfW;
-                    const float dx = (float)(cv[0] - cv[1]);
-                    const float dy = (float)(cv[2] - cv[3]);
-                    const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
-                    const float ob = (atan2_f32(dy, dx) - porif) * (float)(kDescBins / kTwoPi);
-                    const float wgt =
-                        __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
-                    const float m = mag * wgt;
-                    const float fbr = floorf(rb), fbc = floorf(cb), fbo = floorf(ob);
-                    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
-                    const float fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
-#pragma unroll
-                    for (int rq = 0; rq <= 1; ++rq) {
-                        const int ri = br + rq;
-                        if ((unsigned)ri >= (unsigned)kDescW) continue;
-                        const float vr = m * ((rq == 0) ? 1.0f - fr : fr);
-#pragma unroll
-                        for (int cq = 0; cq <= 1; ++cq) {
-                            const int ci = bc + cq;
-                            if ((unsigned)ci >= (unsigned)kDescW) continue;
-                            const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
-                            double* hb = &rep[(ri * 32 + ci * 8) * kDescWReps];
-                            atomicAdd(&hb[(bo & 7) * kDescWReps], (double)(vc * (1.0f - fo)));
-                            atomicAdd(&hb[((bo + 1) & 7) * kDescWReps], (double)(vc * fo));
-                        }
-                    }
-                }
-                srow = qrow[0];
-                scol = qcol[0];
-                cok = qok[0];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) cv[q] = qv[0][q];
-#pragma unroll
-                for (int a = 0; a + 1 < kAhead; ++a) {
-                    qrow[a] = qrow[a + 1];
-                    qcol[a] = qcol[a + 1];
-                    qok[a] = qok[a + 1];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
-                }
-            }
+        for (int cq = 0; cq <= 1; ++cq) {
+            const int ci = bc + cq;
+            if ((unsigned)ci >= (unsigned)kDescW) continue;
+            const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
+            double* hb = &rep[(ri * 32 + ci * 8) * NR];
+            atomicAdd(&hb[(bo & 7) * NR], (double)(vc * (1.0f - fo)));
+            atomicAdd(&hb[((bo + 1) & 7) * NR], (double)(vc * fo));
         }
-        wave_sync();
-        // ---- reduce the replicas (bins lane, lane + 64), normalise, clamp,
-        // renormalise, quantise (sift.cpp:576-603)
-        double v0 = 0.0, v1 = 0.0;
-#pragma unroll
-        for (int q = 0; q < kDescWReps; ++q) {
-            // fixed order per bin, rotated by lane so the 16 lanes of a read
-            // group start on different bank pairs
-            const int r = (q + lane) & (kDescWReps - 1);
-            v0 += hist[lane * kDescWReps + r];
-            v1 += hist[(lane + 64) * kDescWReps + r];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The samples of rows j0, j0 + dj, ... of the window (row j = row - radius),
+// 64 rows per group (lane = row), walked 64 samples per step:
+//  * each lane bounds its row's sample interval: an f32 SUPERSET of the
+//    reference's rotated box (|col sa + row ca| < 2.5 hw and
+//    |col ca - row sa| < 2.5 hw, widened by 0.01 column; f32 rounding of
+//    the bounds is far below that) intersected exactly with the radius and
+//    the image border (sift.cpp:634-656);
+//  * a wave scan of the row lengths, then sample t0 + lane is located by a
+//    branch-free binary search over the 64 inclusive prefixes;
+//  * the next step's four gradient loads per lane are in flight while the
+//    current step's samples are processed (issued unconditionally: lanes
+//    past the end read pixel (1, 1), so the compiler can count them).
+// ---------------------------------------------------------------------------
+template <bool F64, int NR>
+__device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, double* rep,
+                                          const double2* atab) {
+    const int lane = threadIdx.x & 63;
+    const int side = 2 * d.radius + 1;
+    gdouble* img = gbl(d.img);
+    const int W = d.W, H = d.H, x = d.x, y = d.y, radius = d.radius;
+    for (int g0 = j0; g0 < side; g0 += 64 * dj) {
+        const int j = g0 + dj * lane;
+        const int row = j - radius;
+        int lo = 0, len = 0;
+        if (j < side && row + y > 0 && row + y < H - 1) {
+            const float fr = (float)row, ra = fr * d.caf, rs = fr * d.saf;
+            float clo = (float)max(-radius, 1 - x), chi = (float)min(radius, W - 2 - x);
+            if (fabsf(d.saf) > 1e-6f) {
+                const float is = 1.0f / d.saf;
+                const float a1 = (-d.limf - ra) * is, a2 = (d.limf - ra) * is;
+                clo = fmaxf(clo, fminf(a1, a2) - 0.01f);
+                chi = fminf(chi, fmaxf(a1, a2) + 0.01f);
+            } else if (!(fabsf(ra) < d.limf + 0.01f)) {
+                chi = clo - 1.0f;
+            }
+            if (fabsf(d.caf) > 1e-6f) {
+                const float ic = 1.0f / d.caf;
+                const float b1 = (-d.limf + rs) * ic, b2 = (d.limf + rs) * ic;
+                clo = fmaxf(clo, fminf(b1, b2) - 0.01f);
+                chi = fminf(chi, fmaxf(b1, b2) + 0.01f);
+            } else if (!(fabsf(rs) < d.limf + 0.01f)) {
+                chi = clo - 1.0f;
+            }
+            lo = (int)ceilf(clo);
+            const int hi = (int)floorf(chi);
+            len = hi >= lo ? hi - lo + 1 : 0;
         }
-        const double ninv = 1.0 / sqrt(wave_sum_f64(v0 * v0 + v1 * v1));
-        double c0 = v0 * ninv, c1 = v1 * ninv;
-        if (c0 > kMagThr) c0 = kMagThr;
-        if (c1 > kMagThr) c1 = kMagThr;
-        const double inv2 = 1.0 / sqrt(wave_sum_f64(c0 * c0 + c1 * c1));
-        auto quant = [&](double c) -> uint8_t {
-            const double q = floor(kIntFactor * c * inv2);
-            int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
-            return (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
+        int pre = len;  // inclusive scan of the row lengths
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(pre, off);
+            if (lane >= off) pre += t;
+        }
+        const int total = __builtin_amdgcn_readlane(pre, 63);
+        auto locate = [&](int t0, int& srow, int& scol) -> bool {
+            const int t = t0 + lane;
+            int r = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (__shfl(pre, r + step - 1) <= t) r += step;
+            const int lo_r = __shfl(lo, r);
+            const int ex_r = __shfl(pre, r) - __shfl(len, r);
+            srow = g0 + dj * r - radius;
+            scol = lo_r + (t - ex_r);
+            return t < total;
         };
-        const uint8_t u0 = quant(c0), u1 = quant(c1);
-        recs[k].desc[lane] = u0;
-        recs[k].desc[lane + 64] = u1;
-        if (desc_f32) {
-            desc_f32[(size_t)k * 128 + lane] = (float)(c0 * inv2);
-            desc_f32[(size_t)k * 128 + lane + 64] = (float)(c1 * inv2);
-        }
-        if (k < ex.cap) {
-            ex.rec[k].desc[lane] = u0;
-            ex.rec[k].desc[lane + 64] = u1;
-            if (lane == 0) {
-                sift_kp& r = ex.rec[k];
-                r.x = kx;
-                r.y = ky;
-                r.octave = o;
-                r.layer = layer;
-                r.size = ksize;
-                r.pori = pori;
-                ex.side[k] = rside;
+        auto fetch = [&](bool ok, int srow, int scol, double* v) {
+            const size_t r0 = ok ? (size_t)(srow + y) * W + scol + x : (size_t)W + 1;
+            v[0] = img[r0 + 1];
+            v[1] = img[r0 - 1];
+            v[2] = img[r0 - W];
+            v[3] = img[r0 + W];
+        };
+        int srow = 0, scol = 0, nrow = 0, ncol = 0;
+        double cv[4], nv[4];
+        bool cok = total > 0 && locate(0, srow, scol);
+        fetch(cok, srow, scol, cv);
+        for (int t0 = 0; t0 < total; t0 += 64) {
+            nrow = ncol = 0;
+            const bool nok = t0 + 64 < total && locate(t0 + 64, nrow, ncol);
+            fetch(nok, nrow, ncol, nv);
+            if (cok) {
+                if (F64) add_sample_f64<NR>(rep, scol, srow, cv, d, atab);
+                else add_sample_f32<NR>(rep, scol, srow, cv, d);
             }
+            srow = nrow;
+            scol = ncol;
+            cok = nok;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
         }
-        wave_sync();
+    }
+}
+
+// This wave's NR replicas (bin i of replica r at hist[i * NR + r]) -> bins
+// lane and lane + 64, in a fixed order per bin (rotated by lane so the 16
+// lanes of a read group start on different bank pairs)
+template <int NR>
+__device__ __forceinline__ void reduce_replicas(const double* hist, double& v0, double& v1) {
+    const int lane = threadIdx.x & 63;
+    v0 = v1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        const int r = (q + lane) & (NR - 1);
+        v0 += hist[lane * NR + r];
+        v1 += hist[(lane + 64) * NR + r];
+    }
+}
+
+// convert_hist_to_desc (sift.cpp:576-603) of bins lane / lane + 64 of record
+// k, by one wave: normalise, clamp at 0.2, renormalise, quantise; the record
+// and its export copy are written
+__device__ __forceinline__ void finish_record(double v0, double v1, const DescRecord& d,
+                                              unsigned k, sift_kp* __restrict__ recs,
+                                              float* __restrict__ desc_f32,
+                                              const ExportSink& ex) {
+    const int lane = threadIdx.x & 63;
+    const double ninv = 1.0 / sqrt(wave_sum_f64(v0 * v0 + v1 * v1));
+    double c0 = v0 * ninv, c1 = v1 * ninv;
+    if (c0 > kMagThr) c0 = kMagThr;
+    if (c1 > kMagThr) c1 = kMagThr;
+    const double inv2 = 1.0 / sqrt(wave_sum_f64(c0 * c0 + c1 * c1));
+    auto quant = [&](double c) -> uint8_t {
+        const double q = floor(kIntFactor * c * inv2);
+        int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
+        return (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
+    };
+    const uint8_t u0 = quant(c0), u1 = quant(c1);
+    recs[k].desc[lane] = u0;
+    recs[k].desc[lane + 64] = u1;
+    if (desc_f32) {
+        desc_f32[(size_t)k * 128 + lane] = (float)(c0 * inv2);
+        desc_f32[(size_t)k * 128 + lane + 64] = (float)(c1 * inv2);
+    }
+    if (k < ex.cap) {
+        ex.rec[k].desc[lane] = u0;
+        ex.rec[k].desc[lane + 64] = u1;
+        if (lane == 0) {
+            sift_kp& r = ex.rec[k];
+            r.x = d.kx;
+            r.y = d.ky;
+            r.octave = d.o;
+            r.layer = d.layer;
+            r.size = d.ksize;
+            r.pori = d.pori;
+            ex.side[k] = d.side;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
 // k_descriptor_split<F64> (desc_mode 0 with F64, the default): one record
 // per 256-thread workgroup, from the work counter.
-//  * The rows of the window are dealt round-robin to the four waves (row j
-//    of the window to wave j % 4); each wave enumerates its rows' sample
-//    intervals as k_descriptor_wave does (f32 superset of the rotated box,
-//    wave scan, binary-search locate) and walks them 64 samples per step
-//    with the next step's gradient loads in flight. A record takes a quarter
-//    of a wavefront's serial walk (the synchronous latency's tail, DESIGN
-//    §4), and the split depends only on the record, so its bytes do not
-//    depend on how its job was batched.
-//  * F64: the reference's per-sample expressions in f64 (sift.cpp:641-678):
-//    row_rot / col_rot with the correctly rounded division by hist_width,
-//    (row_rot + 2) - 0.5, the gradient, sqrt, atan2 - pori and the two
-//    fmods (exact compare-and-subtract), exp of -(row_rot^2 + col_rot^2)/8,
-//    the trilinear split. Samples of the f32 superset outside the box get
-//    row_bin / col_bin <= -1 or >= 4 from these exact expressions: their
-//    cells are all skipped, or take weight 0 (row_bin = -1 exactly), so the
-//    contributing sample set is exactly the reference's. What differs from
-//    the reference is the last bit of sqrt/atan2/exp/sin/cos (device math,
-//    see above) and the histogram summation order; the normalised floats
-//    agree to ~1e-15.
+//  * Row j of the window goes to wave j % 4 (desc_walk with dj = 4), so a
+//    record takes a quarter of a wavefront's serial walk, and the split
+//    depends only on the record: its bytes do not depend on how its job
+//    was batched.
 //  * Each wave adds into its own kSplitReps lane-interleaved f64 replicas
-//    (ds_add_f64, conflict-free at 16); a wave reduces its replicas to two
-//    bins per lane, and wave 0 sums the four waves' partials in wave order,
-//    normalises, clamps, renormalises and quantises (sift.cpp:576-603).
-//    Fixed order throughout: the bytes depend only on the record.
+//    (ds_add_f64; conflict-free at 16: a lane's bank pair is
+//    2 (i * 16 + r) mod 32, its own whatever bin the sample hits); a wave
+//    reduces its replicas to two bins per lane, wave 0 sums the four waves'
+//    partials in wave order and finishes the record. Fixed order
+//    throughout: the bytes depend only on the record.
+//  * One lane of wave 1 claims the next record (and evaluates the f64
+//    sin / cos of its orientation, once per record) while wave 0 finishes
+//    the current one; two barriers per record.
 // ---------------------------------------------------------------------------
 constexpr int kSplitReps = SIFT_DSPLIT_REPS;
 static_assert(kSplitReps >= 1 && kSplitReps <= 16 && (kSplitReps & (kSplitReps - 1)) == 0,
@@ -392,11 +402,12 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kSplitReps];
     __shared__ double2 atab[17];
     __shared__ unsigned next_k;
+    __shared__ double2 next_sc;  // sin, cos of the next record's pori (F64)
     set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double* const hist = hist_all + wv * 128 * kSplitReps;
-    double* const rep = hist + (lane & (kSplitReps - 1));  // bin i at rep[i * kSplitReps]
+    double* const rep = hist + (lane & (kSplitReps - 1));
     const unsigned n = min(*n_rec, cap_rec);
     const unsigned k0 = min(*rec_begin, n);
     // the launch's record range is fixed before it starts (orientation has
@@ -406,254 +417,96 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
         ex.cnt[1] = n;
     }
     if (threadIdx.x < 17) atab[threadIdx.x] = kAtanTab[threadIdx.x];
-    if (threadIdx.x == 0) next_k = atomicAdd(work, 1u);
+    auto claim_next = [&]() {
+        const unsigned c = atomicAdd(work, 1u);
+        next_k = c;
+        if (F64 && k0 + c < n) {
+            const double pr = recs[k0 + c].pori;
+            next_sc = make_double2(sin(pr), cos(pr));
+        }
+    };
+    if (threadIdx.x == 0) claim_next();
     __syncthreads();
-    constexpr float kHalfW = (float)(kDescW / 2 - 0.5);
-    const float wscale = (float)(-1.4426950408889634 / (0.5 * kDescW * kDescW));
-    constexpr double kBinsPerRad = kDescBins / kTwoPi;  // sift.cpp:628
     for (;;) {
         const unsigned k = k0 + next_k;
         if (k >= n) break;
-        // ---- record setup (wave-uniform, every wave)
-        const sift_kp& R = recs[k];
-        const double kx = R.x, ky = R.y, ksize = R.size, pori = R.pori;
-        const int o = R.octave, layer = R.layer;
-        const RecSide rside = rec_side[k];
-        gdouble* img = gbl(plane(pt, rside.img, o, layer));
-        const int W = pt->w[o], H = pt->h[o];
-        const double inv = P.double_image ? (1.0 / pow2i(o - 1)) : (1.0 / pow2i(o));
-        const int x = (int)(kx * inv);
-        const int y = (int)(ky * inv);
-        const double hw = P.desc_scale_factor * (ksize * inv);
-        const double rr = round(hw * 0.5 * sqrt(2.0) * (kDescW + 1.0) + 0.5);
-        const double diag = sqrt((double)(W * W + H * H));
-        const int radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
-        const int side = 2 * radius + 1;
-        const double ihw = 1.0 / hw;
-        double sa = 0.0, ca = 1.0;
-        if (F64) {
-            sa = sin(pori);
-            ca = cos(pori);
-        }
-        float saf, caf;
-        if (F64) {
-            saf = (float)sa;
-            caf = (float)ca;
-        } else {
-            sincosf((float)pori, &saf, &caf);
-        }
-        const float ihwf = (float)ihw;
-        const float porif = (float)pori;
-        const float limf = (float)((0.5 * kDescW + 0.5) * hw);  // |rot| < 2.5 hw
+        const double2 sc = next_sc;
+        const DescRecord d = load_record<F64>(pt, P, recs[k], rec_side[k], &sc);
         for (int i = lane; i < 64 * kSplitReps; i += 64)
             reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
         wave_sync();
-        // ---- this wave's rows j = wv + 4 i, 64 of them (lane = row) per group
-        for (int g0 = wv; g0 < side; g0 += 4 * 64) {
-            const int j = g0 + 4 * lane;
-            const int row = j - radius;
-            int lo = 0, len = 0;
-            if (j < side && row + y > 0 && row + y < H - 1) {
-                const float fr = (float)row, ra = fr * caf, rs = fr * saf;
-                float clo = (float)max(-radius, 1 - x), chi = (float)min(radius, W - 2 - x);
-                // |c sa + r ca| < lim and |c ca - r sa| < lim, widened by 0.01
-                // column (f32 rounding of the bounds is far below that)
-                if (fabsf(saf) > 1e-6f) {
-                    const float is = 1.0f / saf;
-                    const float a1 = (-limf - ra) * is, a2 = (limf - ra) * is;
-                    clo = fmaxf(clo, fminf(a1, a2) - 0.01f);
-                    chi = fminf(chi, fmaxf(a1, a2) + 0.01f);
-                } else if (!(fabsf(ra) < limf + 0.01f)) {
-                    chi = clo - 1.0f;
-                }
-                if (fabsf(caf) > 1e-6f) {
-                    const float ic = 1.0f / caf;
-                    const float b1 = (-limf + rs) * ic, b2 = (limf + rs) * ic;
-                    clo = fmaxf(clo, fminf(b1, b2) - 0.01f);
-                    chi = fminf(chi, fmaxf(b1, b2) + 0.01f);
-                } else if (!(fabsf(rs) < limf + 0.01f)) {
-                    chi = clo - 1.0f;
-                }
-                lo = (int)ceilf(clo);
-                const int hi = (int)floorf(chi);
-                len = hi >= lo ? hi - lo + 1 : 0;
-            }
-            int pre = len;  // inclusive scan of the row lengths
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int t = __shfl_up(pre, off);
-                if (lane >= off) pre += t;
-            }
-            const int total = __builtin_amdgcn_readlane(pre, 63);
-            // (row, col) of sample t0 + lane: its row r is the number of rows
-            // whose inclusive prefix is <= t (branch-free binary search)
-            auto locate = [&](int t0, int& srow, int& scol) -> bool {
-                const int t = t0 + lane;
-                int r = 0;
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (__shfl(pre, r + step - 1) <= t) r += step;
-                const int lo_r = __shfl(lo, r);
-                const int ex_r = __shfl(pre, r) - __shfl(len, r);
-                srow = g0 + 4 * r - radius;
-                scol = lo_r + (t - ex_r);
-                return t < total;
-            };
-            // gradient loads issued unconditionally (lanes past the end read
-            // pixel (1, 1)) so the compiler can count them
-            auto fetch = [&](bool ok, int srow, int scol, double* v) {
-                const size_t r0 = ok ? (size_t)(srow + y) * W + scol + x : (size_t)W + 1;
-                v[0] = img[r0 + 1];
-                v[1] = img[r0 - 1];
-                v[2] = img[r0 - W];
-                v[3] = img[r0 + W];
-            };
-            int srow = 0, scol = 0, nrow = 0, ncol = 0;
-            double cv[4], nv[4];
-            bool cok = total > 0 && locate(0, srow, scol);
-            fetch(cok, srow, scol, cv);
-            for (int t0 = 0; t0 < total; t0 += 64) {
-                // the next block's loads are in flight while this one is processed
-                nrow = ncol = 0;
-                const bool nok = t0 + 64 < total && locate(t0 + 64, nrow, ncol);
-                fetch(nok, nrow, ncol, nv);
-                if (F64 && cok) {
-                    const double dcol = (double)scol, drow = (double)srow;
-                    const double row_rot = div_sum_w(dcol * sa + drow * ca, hw, ihw);
-                    const double col_rot = div_sum_w(dcol * ca - drow * sa, hw, ihw);
-                    const double rb = row_rot + kDescW / 2 - 0.5;
-                    const double cb = col_rot + kDescW / 2 - 0.5;
-                    const double dx = cv[0] - cv[1];
-                    const double dy = cv[2] - cv[3];
-                    const double mag = sqrt_f64(dx * dx + dy * dy);
-                    double ang = atan2_f64(dy, dx, atab) - pori;
-                    // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi:
-                    // fmod(a, M) = a - trunc(a/M) M is exact here, so
-                    // compare-and-subtract reproduces it bit for bit
-                    if (ang >= kTwoPi) ang -= kTwoPi;
-                    else if (ang <= -kTwoPi) ang += kTwoPi;
-                    ang += kTwoPi;
-                    if (ang >= kTwoPi) ang -= kTwoPi;
-                    if (ang >= kTwoPi) ang -= kTwoPi;
-                    const double ob = ang * kBinsPerRad;
-                    const double wgt =
-                        exp_f64(-(row_rot * row_rot + col_rot * col_rot) / (0.5 * kDescW * kDescW));
-                    const double m = mag * wgt;
-                    const double fbr = floor(rb), fbc = floor(cb), fbo = floor(ob);
-                    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
-                    const double fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
-#pragma unroll
-                    for (int rq = 0; rq <= 1; ++rq) {
-                        const int ri = br + rq;
-                        if ((unsigned)ri >= (unsigned)kDescW) continue;
-                        const double vr = m * ((rq == 0) ? 1.0 - fr : fr);
-#pragma unroll
-                        for (int cq = 0; cq <= 1; ++cq) {
-                            const int ci = bc + cq;
-                            if ((unsigned)ci >= (unsigned)kDescW) continue;
-                            const double vc = vr * ((cq == 0) ? 1.0 - fc : fc);
-                            double* hb = &rep[(ri * 32 + ci * 8) * kSplitReps];
-                            atomicAdd(&hb[(bo & 7) * kSplitReps], vc * (1.0 - fo));
-                            atomicAdd(&hb[((bo + 1) & 7) * kSplitReps], vc * fo);
-                        }
-                    }
-                } else if (!F64 && cok) {
-                    const float fcol = (float)scol, frow = (float)srow;
-                    const float row_rot = fmaf(fcol, saf, frow * caf) * ihwf;
-                    const float col_rot = fmaf(fcol, caf, -(frow * saf)) * ihwf;
-                    const float rb = row_rot + kHalfW;
-                    const float cb = col_rot + kHalfW;
-                    const float dx = (float)(cv[0] - cv[1]);
-                    const float dy = (float)(cv[2] - cv[3]);
-                    const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
-                    const float ob = (atan2_f32(dy, dx) - porif) * (float)(kDescBins / kTwoPi);
-                    const float wgt =
-                        __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
-                    const float m = mag * wgt;
-                    const float fbr = floorf(rb), fbc = floorf(cb), fbo = floorf(ob);
-                    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
-                    const float fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
-#pragma unroll
-                    for (int rq = 0; rq <= 1; ++rq) {
-                        const int ri = br + rq;
-                        if ((unsigned)ri >= (unsigned)kDescW) continue;
-                        const float vr = m * ((rq == 0) ? 1.0f - fr : fr);
-#pragma unroll
-                        for (int cq = 0; cq <= 1; ++cq) {
-                            const int ci = bc + cq;
-                            if ((unsigned)ci >= (unsigned)kDescW) continue;
-                            const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
-                            double* hb = &rep[(ri * 32 + ci * 8) * kSplitReps];
-                            atomicAdd(&hb[(bo & 7) * kSplitReps], (double)(vc * (1.0f - fo)));
-                            atomicAdd(&hb[((bo + 1) & 7) * kSplitReps], (double)(vc * fo));
-                        }
-                    }
-                }
-                srow = nrow;
-                scol = ncol;
-                cok = nok;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) cv[q] = nv[q];
-            }
-        }
+        desc_walk<F64, kSplitReps>(d, wv, 4, rep, atab);
         wave_sync();
-        // ---- this wave's replicas -> bins lane, lane + 64 (fixed order per
-        // bin, rotated by lane so the 16 lanes of a read group start on
-        // different bank pairs), parked at the front of its own region
-        double v0 = 0.0, v1 = 0.0;
-#pragma unroll
-        for (int q = 0; q < kSplitReps; ++q) {
-            const int r = (q + lane) & (kSplitReps - 1);
-            v0 += hist[lane * kSplitReps + r];
-            v1 += hist[(lane + 64) * kSplitReps + r];
-        }
+        double v0, v1;
+        reduce_replicas<kSplitReps>(hist, v0, v1);
         wave_sync();
-        hist[lane] = v0;
+        hist[lane] = v0;  // this wave's partial, parked at the front of its region
         hist[lane + 64] = v1;
         __syncthreads();
         if (wv == 0) {
-            // the four waves' partials in wave order; normalise, clamp,
-            // renormalise, quantise (sift.cpp:576-603)
 #pragma unroll
-            for (int w = 1; w < 4; ++w) {
+            for (int w = 1; w < 4; ++w) {  // the partials in wave order
                 v0 += hist_all[w * 128 * kSplitReps + lane];
                 v1 += hist_all[w * 128 * kSplitReps + lane + 64];
             }
-            const double ninv = 1.0 / sqrt(wave_sum_f64(v0 * v0 + v1 * v1));
-            double c0 = v0 * ninv, c1 = v1 * ninv;
-            if (c0 > kMagThr) c0 = kMagThr;
-            if (c1 > kMagThr) c1 = kMagThr;
-            const double inv2 = 1.0 / sqrt(wave_sum_f64(c0 * c0 + c1 * c1));
-            auto quant = [&](double c) -> uint8_t {
-                const double q = floor(kIntFactor * c * inv2);
-                int val = (q == q) ? (int)q : 0;  // NaN -> 0 (Appendix A.17)
-                return (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
-            };
-            const uint8_t u0 = quant(c0), u1 = quant(c1);
-            recs[k].desc[lane] = u0;
-            recs[k].desc[lane + 64] = u1;
-            if (desc_f32) {
-                desc_f32[(size_t)k * 128 + lane] = (float)(c0 * inv2);
-                desc_f32[(size_t)k * 128 + lane + 64] = (float)(c1 * inv2);
-            }
-            if (k < ex.cap) {
-                ex.rec[k].desc[lane] = u0;
-                ex.rec[k].desc[lane + 64] = u1;
-                if (lane == 0) {
-                    sift_kp& r = ex.rec[k];
-                    r.x = kx;
-                    r.y = ky;
-                    r.octave = o;
-                    r.layer = layer;
-                    r.size = ksize;
-                    r.pori = pori;
-                    ex.side[k] = rside;
-                }
-            }
+            finish_record(v0, v1, d, k, recs, desc_f32, ex);
         } else if (wv == 1 && lane == 0) {
-            next_k = atomicAdd(work, 1u);  // the next record, while wave 0 finishes
+            claim_next();
         }
         __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_descriptor_wave<F64> (A/B: desc_mode 1 f32, 3 f64): one WAVEFRONT per
+// record, four independent waves per workgroup pulling records from the work
+// counter; no workgroup barrier anywhere (a wave's LDS instructions execute
+// in order, so zeroing -> accumulation -> reduction -> next record's zeroing
+// needs only compiler ordering, wave_sync). A record's samples are one
+// wave's serial walk.
+// ---------------------------------------------------------------------------
+constexpr int kDescWReps = SIFT_DESCW_REPS;
+static_assert(kDescWReps >= 1 && kDescWReps <= 16 && (kDescWReps & (kDescWReps - 1)) == 0,
+              "replicas: a power of two <= 16");
+
+template <bool F64>
+__global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
+    const PyrTable* __restrict__ pt, DevParams P, sift_kp* __restrict__ recs,
+    const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
+    const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
+    unsigned* __restrict__ work, ExportSink ex) {
+    __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kDescWReps];
+    __shared__ double2 atab[17];
+    set_job_prio(pt->jp, 0);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double* const hist = hist_all + wv * 128 * kDescWReps;
+    double* const rep = hist + (lane & (kDescWReps - 1));
+    const unsigned n = min(*n_rec, cap_rec);
+    const unsigned k0 = min(*rec_begin, n);
+    if (ex.cnt && blockIdx.x == 0 && threadIdx.x == 0) {
+        ex.cnt[0] = k0;
+        ex.cnt[1] = n;
+    }
+    if (F64) {
+        if (threadIdx.x < 17) atab[threadIdx.x] = kAtanTab[threadIdx.x];
+        __syncthreads();  // the only barrier, before any wave can leave
+    }
+    for (;;) {
+        unsigned claim = 0;
+        if (lane == 0) claim = atomicAdd(work, 1u);
+        const unsigned k = k0 + __builtin_amdgcn_readfirstlane(claim);
+        if (k >= n) break;
+        const DescRecord d = load_record<F64>(pt, P, recs[k], rec_side[k], nullptr);
+        for (int i = lane; i < 64 * kDescWReps; i += 64)
+            reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
+        wave_sync();
+        desc_walk<F64, kDescWReps>(d, 0, 1, rep, atab);
+        wave_sync();
+        double v0, v1;
+        reduce_replicas<kDescWReps>(hist, v0, v1);
+        finish_record(v0, v1, d, k, recs, desc_f32, ex);
+        wave_sync();
     }
 }
 
@@ -664,11 +517,12 @@ hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* 
                              const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
                              unsigned* work, const ExportSink& ex, unsigned wgs,
                              int mode, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    // persistent: workgroups pull records
-    if (mode == 1) {  // four waves per workgroup, a record per wave (f32 sample math)
+    // persistent grids: workgroups pull records
+    if (mode == 1 || mode == 3) {  // a record per wave, four waves per workgroup
         const unsigned blocks = std::min<unsigned>(wgs, cap_rec > 0 ? (cap_rec + 3) / 4 : 1);
-        return launch_timed(k_descriptor_wave, dim3(blocks), dim3(256), 0, s, e0, e1, d_pt, P,
-                            recs, rec_side, rec_begin, n_rec, cap_rec, desc_f32, work, ex);
+        auto kern = mode == 3 ? k_descriptor_wave<true> : k_descriptor_wave<false>;
+        return launch_timed(kern, dim3(blocks), dim3(256), 0, s, e0, e1, d_pt, P, recs, rec_side,
+                            rec_begin, n_rec, cap_rec, desc_f32, work, ex);
     }
     const unsigned blocks = std::min<unsigned>(wgs, cap_rec > 0 ? cap_rec : 1);
     auto kern = mode == 2 ? k_descriptor_split<false> : k_descriptor_split<true>;

@@ -264,7 +264,8 @@ def test_gpu_pyramid_paths_match_oracle(lds_px, shape):
 
 # Descriptor variants (SIFT_DESC_MODE): 0 = k_descriptor_split with f64
 # sample math (default), 1 = k_descriptor_wave (a wavefront per record, f32
-# sample math), 2 = k_descriptor_split with f32 sample math. Each must meet
+# sample math), 2 = k_descriptor_split with f32 sample math, 3 = k_descriptor_wave
+# with f64 sample math. Each must meet
 # the descriptor contract on the 1080p golden and on the stb-decoded
 # photographs (natural gradients).
 DESC_GOLDENS = [g for g in GOLDENS if g.name in ("synth_1920x1080", "image1",
@@ -283,7 +284,7 @@ def test_gpu_descriptor_f64_reference_precision(gpu_ctx, g):
     assert r["desc_u8_mismatch"] == 0 and r["desc_f32_max"] <= DESC_F64_F32_TOL, r
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("g", DESC_GOLDENS, ids=[g.name for g in DESC_GOLDENS])
 def test_gpu_descriptor_modes_match_golden(mode, g):
     import os

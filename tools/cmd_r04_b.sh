@@ -1,0 +1,17 @@
+#!/bin/bash
+# descriptor variants: parity of every mode, kernel-alone times + latency, pipelined A/B
+set -o pipefail
+O=gpurun_out/r04_b
+mkdir -p $O
+L=sift-project_amd/alt/reps8/libsift_hip.so
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread \
+    -k "descriptor or deterministic" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 400 python -u tools/kernel_alone.py --n 40 base SIFT_DESC_MODE=1 SIFT_DESC_MODE=2 SIFT_DESC_MODE=3 \
+    SIFT_DESC_WGS=384 SIFT_HIP_LIB=$L SIFT_HIP_LIB=$L,SIFT_DESC_WGS=384 SIFT_LDS_PX=2100 \
+    > $O/alone.txt 2>&1 || { tail -20 $O/alone.txt; exit 1; }
+grep -v amdgpu.ids $O/alone.txt
+timeout -k 10 700 python -u tools/ab_interleaved.py --rounds 6 --steps 200 base SIFT_DESC_MODE=3 SIFT_DESC_WGS=384 \
+    SIFT_HIP_LIB=$L SIFT_HIP_LIB=$L,SIFT_DESC_WGS=384 SIFT_DESC_MODE=1 SIFT_LDS_PX=2100 \
+    > $O/ab.txt 2>&1 || { tail -20 $O/ab.txt; exit 1; }
+grep -v amdgpu.ids $O/ab.txt
