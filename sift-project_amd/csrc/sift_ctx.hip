@@ -251,7 +251,7 @@ struct sift_ctx {
     // 1024 workgroups starved the concurrent small-octave blurs on its
     // critical path. SIFT_KP_WGS / SIFT_DESC_WGS (tuning).
     unsigned kp_wgs = 192;
-    unsigned desc_wgs = 192;
+    unsigned desc_wgs = 384;  // k_descriptor_split: ONE record per workgroup
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
     // rest form one final batch after the LDS octaves. A single-image job
     // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
@@ -264,7 +264,7 @@ struct sift_ctx {
     int batch_px_log2_alone = 18;
     // octaves of at most this many pixels (and within the LDS, lds_octave_fits)
     // run LDS-resident in the one-workgroup k_octaves_lds (SIFT_LDS_PX, tests)
-    size_t lds_max_px = kLdsOctavePx;
+    size_t lds_max_px = kLdsOctaveMaxPx;
     bool serial = false;  // SIFT_SERIAL=1: every kernel on one stream (profiling)
     // Kernels raise their waves' issue priority by their job's age rank
     // (JobPrio; -1.3 % on the driver's bench command, round 3); d_done

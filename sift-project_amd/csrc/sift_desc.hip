@@ -21,10 +21,10 @@
 // replicas of the 4x4x8 f64 histogram per wave (power of two <= 16) and the
 // minimum workgroups per CU, per kernel shape
 #ifndef SIFT_DSPLIT_REPS
-#define SIFT_DSPLIT_REPS 16
+#define SIFT_DSPLIT_REPS 8
 #endif
 #ifndef SIFT_DSPLIT_OCC
-#define SIFT_DSPLIT_OCC (SIFT_DSPLIT_REPS >= 16 ? 2 : 4)
+#define SIFT_DSPLIT_OCC (SIFT_DSPLIT_REPS >= 16 ? 2 : 3)
 #endif
 #ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
 #define SIFT_DESCW_REPS 16
@@ -142,7 +142,8 @@ __device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevP
 // ---------------------------------------------------------------------------
 template <int NR>
 __device__ __forceinline__ void add_sample_f64(double* rep, int scol, int srow, const double* cv,
-                                               const DescRecord& d, const double2* atab) {
+                                               const DescRecord& d, const double2* atab,
+                                               const double* gtab) {
     constexpr double kBinsPerRad = kDescBins / kTwoPi;  // sift.cpp:628
     const double dcol = (double)scol, drow = (double)srow;
     const double row_rot = div_sum_w(dcol * d.sa + drow * d.ca, d.hw, d.ihw);
@@ -153,15 +154,21 @@ __device__ __forceinline__ void add_sample_f64(double* rep, int scol, int srow, 
     const double dy = cv[2] - cv[3];
     const double mag = sqrt_f64(dx * dx + dy * dy);
     double ang = atan2_f64(dy, dx, atab) - d.pori;
-    // fmod(fmod(ang, 2pi) + 2pi, 2pi) with |ang| < 2 * 2pi: fmod(a, M) =
-    // a - trunc(a/M) M is exact here, so compare-and-subtract reproduces it
-    if (ang >= kTwoPi) ang -= kTwoPi;
-    else if (ang <= -kTwoPi) ang += kTwoPi;
+    // fmod(fmod(ang, 2pi) + 2pi, 2pi): atan2 in [-pi, pi] and pori in
+    // [0, 2pi) put ang in (-3pi, pi], so the inner fmod only adds 2pi when
+    // ang <= -2pi and the outer one only subtracts 2pi once; both exact
+    // (Sterbenz), so compare-and-add reproduces them bit for bit
+    if (ang <= -kTwoPi) ang += kTwoPi;
     ang += kTwoPi;
     if (ang >= kTwoPi) ang -= kTwoPi;
-    if (ang >= kTwoPi) ang -= kTwoPi;
     const double ob = ang * kBinsPerRad;
-    const double wgt = exp_f64(-(row_rot * row_rot + col_rot * col_rot) / (0.5 * kDescW * kDescW));
+    // exp(-(row_rot^2 + col_rot^2) / 8): with the per-record table the
+    // separable form G(row) G(col), G(i) = exp(-i^2 / (8 hw^2)) (rotation
+    // keeps row_rot^2 + col_rot^2 = (row^2 + col^2) / hw^2; the two
+    // evaluations differ by a few 1e-16 relative)
+    const double wgt =
+        gtab ? gtab[srow < 0 ? -srow : srow] * gtab[scol < 0 ? -scol : scol]
+             : exp_f64(-(row_rot * row_rot + col_rot * col_rot) / (0.5 * kDescW * kDescW));
     const double m = mag * wgt;
     const double fbr = floor(rb), fbc = floor(cb), fbo = floor(ob);
     const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
@@ -237,7 +244,7 @@ __device__ __forceinline__ void add_sample_f32(double* rep, int scol, int srow, 
 // ---------------------------------------------------------------------------
 template <bool F64, int NR>
 __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, double* rep,
-                                          const double2* atab) {
+                                          const double2* atab, const double* gtab) {
     const int lane = threadIdx.x & 63;
     const int side = 2 * d.radius + 1;
     gdouble* img = gbl(d.img);
@@ -304,7 +311,7 @@ __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, d
             const bool nok = t0 + 64 < total && locate(t0 + 64, nrow, ncol);
             fetch(nok, nrow, ncol, nv);
             if (cok) {
-                if (F64) add_sample_f64<NR>(rep, scol, srow, cv, d, atab);
+                if (F64) add_sample_f64<NR>(rep, scol, srow, cv, d, atab, gtab);
                 else add_sample_f32<NR>(rep, scol, srow, cv, d);
             }
             srow = nrow;
@@ -390,6 +397,10 @@ __device__ __forceinline__ void finish_record(double v0, double v1, const DescRe
 //    the current one; two barriers per record.
 // ---------------------------------------------------------------------------
 constexpr int kSplitReps = SIFT_DSPLIT_REPS;
+// Gaussian weight table G(0..radius) of the current record (split kernel,
+// F64): one exp per thread per record instead of one per sample; records
+// with a larger radius evaluate exp per sample
+constexpr int kGTab = 256;
 static_assert(kSplitReps >= 1 && kSplitReps <= 16 && (kSplitReps & (kSplitReps - 1)) == 0,
               "replicas: a power of two <= 16");
 
@@ -403,6 +414,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     __shared__ double2 atab[17];
     __shared__ unsigned next_k;
     __shared__ double2 next_sc;  // sin, cos of the next record's pori (F64)
+    __shared__ double gtab[kGTab];
     set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -432,10 +444,16 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
         if (k >= n) break;
         const double2 sc = next_sc;
         const DescRecord d = load_record<F64>(pt, P, recs[k], rec_side[k], &sc);
+        const bool use_tab = F64 && d.radius < kGTab;
+        if (use_tab && (int)threadIdx.x <= d.radius) {
+            const double i = (double)threadIdx.x;
+            gtab[threadIdx.x] = exp_f64(-(i * i) / (0.5 * kDescW * kDescW * d.hw * d.hw));
+        }
         for (int i = lane; i < 64 * kSplitReps; i += 64)
             reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
-        wave_sync();
-        desc_walk<F64, kSplitReps>(d, wv, 4, rep, atab);
+        if (F64) __syncthreads();  // the table (uniform: every thread gets here)
+        else wave_sync();
+        desc_walk<F64, kSplitReps>(d, wv, 4, rep, atab, use_tab ? gtab : nullptr);
         wave_sync();
         double v0, v1;
         reduce_replicas<kSplitReps>(hist, v0, v1);
@@ -501,7 +519,7 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
         for (int i = lane; i < 64 * kDescWReps; i += 64)
             reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
         wave_sync();
-        desc_walk<F64, kDescWReps>(d, 0, 1, rep, atab);
+        desc_walk<F64, kDescWReps>(d, 0, 1, rep, atab, nullptr);
         wave_sync();
         double v0, v1;
         reduce_replicas<kDescWReps>(hist, v0, v1);

@@ -31,6 +31,10 @@ constexpr int kMaxBins = 256;     // orientation bins supported
 // octaves of at most this many pixels run LDS-resident: level + temporary +
 // quarter-size next base = 2.25 * 9088 * 8 B = 163,584 B of the 163,840 B LDS
 constexpr int kLdsOctavePx = 9088;
+// ... by default only octaves of at most this many pixels run there (1080p:
+// 60x33 and smaller; 120x67 as per-level tile launches on several CUs:
+// -2.5 % pipelined, 76 -> 23 + 48 us alone, round 4)
+constexpr int kLdsOctaveMaxPx = 2100;
 constexpr size_t kLdsOctaveBytes = (2 * (size_t)kLdsOctavePx + kLdsOctavePx / 4) * sizeof(double);
 // planes live in LDS with an odd row stride (W | 1 doubles: lane-per-row
 // accesses spread over the banks); an octave fits when its level and the
