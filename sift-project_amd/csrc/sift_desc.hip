@@ -37,32 +37,6 @@ namespace sift_amd {
 
 namespace {
 
-// atan2 in f32 for the f32 sample math: octant reduction to
-// a = min(|x|, |y|) / max(|x|, |y|) (v_rcp_f32, 1 ulp), atan(a) as
-// a + a^3 p(a^2) with a degree-7 p fitted for minimum max error on [0, 1]
-// (8.5e-8 rad in f32 arithmetic over 2e6 points), then the quadrant fix-up.
-// About 20 VALU instructions against ~35 for atan2f; total error below
-// 2e-7 rad, i.e. < 3e-7 of a descriptor orientation bin (contract: 1e-4 on
-// the normalised floats). atan2(0, 0) = 0; signs of zeros as atan2f.
-__device__ __forceinline__ float atan2_f32(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
-    const float t = a * a;
-    float p = 0.0026222362648695707f;
-    p = fmaf(p, t, -0.015132501721382141f);
-    p = fmaf(p, t, 0.04112179949879646f);
-    p = fmaf(p, t, -0.0736670047044754f);
-    p = fmaf(p, t, 0.1057392954826355f);
-    p = fmaf(p, t, -0.1418597400188446f);
-    p = fmaf(p, t, 0.1999039649963379f);
-    p = fmaf(p, t, -0.33332985639572144f);
-    float th = fmaf(a * t, p, a);
-    if (ay > ax) th = 1.57079637f - th;
-    if (x < 0.0f) th = 3.14159274f - th;
-    return copysignf(th, y);
-}
-
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);

@@ -22,6 +22,7 @@
 
 #include "sift_pow2.h"
 #include "sift_device.h"
+#include "sift_math64.h"
 #include "sift_kernels.h"
 
 // compile-time A/B knobs (alternative builds, SIFT_HIP_LIB)
@@ -42,6 +43,9 @@
 #endif
 #ifndef SIFT_PRIO_LDS
 #define SIFT_PRIO_LDS 1
+#endif
+#ifndef SIFT_ORI_FAST  // k_orient_wave: sqrt_f64 + atan2_f32 (0: ocml sqrt + atan2f, A/B)
+#define SIFT_ORI_FAST 1
 #endif
 #ifndef SIFT_EXT_PF
 #define SIFT_EXT_PF 2  // k_extrema_stream: rows in flight
@@ -1112,7 +1116,8 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 // keypoints from the work counter; no workgroup barrier.
 //  * The (2r+1)^2 window is swept 64 samples at a time (lanes along x, so
 //    the four gradient loads coalesce).
-//  * The bin of a sample comes from an f32 atan2f; whenever it lies within
+//  * The bin of a sample comes from an f32 atan2 (atan2_f32, error below
+//    2e-7 rad) and a correctly rounded sqrt; whenever it lies within
 //    nb * 3e-6 of a rounding boundary (10x the f32 path's error bound) or
 //    |dx|, |dy| is tiny, the f64 atan2 decides, so the bin index equals the
 //    f64 one. Gaussian weights come from a per-keypoint table of the same
@@ -1219,11 +1224,16 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             if (cok) {
                 const double dx = cv[0] - cv[1];
                 const double dy = cv[2] - cv[3];
+#if SIFT_ORI_FAST
+                const double mag = sqrt_f64(dx * dx + dy * dy);  // correctly rounded
+                const float at = atan2_f32((float)dy, (float)dx);
+#else
                 const double mag = sqrt(dx * dx + dy * dy);
+                const float at = atan2f((float)dy, (float)dx);
+#endif
                 const int k2 = ci_ * ci_ + cj_ * cj_;
                 const double wgt = use_tab ? wtab[k2] : exp(-k2 / denom);
-                const float t = nbf * (atan2f((float)dy, (float)dx) + (float)kPi) *
-                                (float)(1.0 / kTwoPi);
+                const float t = nbf * (at + (float)kPi) * (float)(1.0 / kTwoPi);
                 int hidx = (int)rintf(t);
                 const bool tiny = (dx != 0.0 && fabs(dx) < 1e-30) || (dy != 0.0 && fabs(dy) < 1e-30);
                 if (fabs((double)t - floor((double)t) - 0.5) < bin_guard || tiny)

@@ -10,6 +10,7 @@
 // Built by __graft_entry__.build(); run by tests/test_gpu_math64.py.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -17,6 +18,7 @@
 #include <cstring>
 #include <vector>
 
+#include "../sift-project_amd/csrc/sift_device.h"
 #include "../sift-project_amd/csrc/sift_math64.h"
 
 using namespace sift_amd;
@@ -34,9 +36,12 @@ __global__ void k_eval(const double* a, const double* b, int n, double* mine, do
     } else if (fn == 1) {
         mine[i] = atan2_f64(a[i], b[i], tab);
         dev[i] = atan2(a[i], b[i]);
-    } else {
+    } else if (fn == 2) {
         mine[i] = exp_f64(a[i]);
         dev[i] = exp(a[i]);
+    } else {  // the f32 atan2 of the orientation bins, error in radians
+        mine[i] = (double)atan2_f32((float)a[i], (float)b[i]);
+        dev[i] = atan2(a[i], b[i]);
     }
 }
 
@@ -68,8 +73,8 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "hipMalloc failed\n");
         return 1;
     }
-    const char* names[3] = {"sqrt", "atan2", "exp"};
-    for (int fn = 0; fn < 3; ++fn) {
+    const char* names[4] = {"sqrt", "atan2", "exp", "atan2_f32"};
+    for (int fn = 0; fn < 4; ++fn) {
         for (int i = 0; i < n; ++i) {
             if (fn == 2) {
                 a[i] = -1.6 * uni();
@@ -104,6 +109,12 @@ int main(int argc, char** argv) {
             hipMemcpy(dev.data(), dd, n * 8, hipMemcpyDeviceToHost)) {
             std::fprintf(stderr, "kernel failed\n");
             return 1;
+        }
+        if (fn == 3) {
+            double emax = 0.0;
+            for (int i = 0; i < n; ++i) emax = std::max(emax, std::fabs(mine[i] - dev[i]));
+            std::printf("%s n=%d abs_err_max_rad=%.3e\n", names[fn], n, emax);
+            continue;
         }
         int64_t umax_dev = 0, umax_ref = 0;
         long ndiff_dev = 0, ndiff_ref = 0;
