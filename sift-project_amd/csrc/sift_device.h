@@ -87,9 +87,10 @@ __device__ __forceinline__ double div_sum_w(double a, double s, double inv) {
 // a + a^3 p(a^2) with a degree-7 p fitted for minimum max error on [0, 1]
 // (8.5e-8 rad in f32 arithmetic over 2e6 points), then the quadrant fix-up.
 // About 20 VALU instructions against ~35 for atan2f; total error below
-// 2e-7 rad (checked against f64 atan2 by tests/test_gpu_math64.py). That
-// is < 3e-7 of a descriptor orientation bin and < 1.2e-6 of an orientation
-// bin at 36 bins, far inside k_orient_wave's guard band. atan2(0, 0) = 0;
+// 3.1e-7 rad with the f32 rounding of the inputs and of the result (checked
+// against f64 atan2 on 4M gradients by tests/test_gpu_math64.py). That is
+// < 4e-7 of a descriptor orientation bin and < 2e-6 of an orientation bin
+// at 36 bins, far inside k_orient_wave's guard band (1e-4 of a bin). atan2(0, 0) = 0;
 // signs of zeros as atan2f.
 __device__ __forceinline__ float atan2_f32(float y, float x) {
     const float ax = fabsf(x), ay = fabsf(y);

@@ -1117,7 +1117,7 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 //  * The (2r+1)^2 window is swept 64 samples at a time (lanes along x, so
 //    the four gradient loads coalesce).
 //  * The bin of a sample comes from an f32 atan2 (atan2_f32, error below
-//    2e-7 rad) and a correctly rounded sqrt; whenever it lies within
+//    3.1e-7 rad) and a correctly rounded sqrt; whenever it lies within
 //    nb * 3e-6 of a rounding boundary (10x the f32 path's error bound) or
 //    |dx|, |dy| is tiny, the f64 atan2 decides, so the bin index equals the
 //    f64 one. Gaussian weights come from a per-keypoint table of the same
