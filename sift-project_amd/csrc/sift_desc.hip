@@ -26,6 +26,9 @@
 #ifndef SIFT_DSPLIT_OCC
 #define SIFT_DSPLIT_OCC (SIFT_DSPLIT_REPS >= 16 ? 2 : 3)
 #endif
+#ifndef SIFT_DESC_AHEAD  // steps of 64 samples whose gradient loads are in flight
+#define SIFT_DESC_AHEAD 2
+#endif
 #ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
 #define SIFT_DESCW_REPS 16
 #endif
@@ -212,9 +215,10 @@ __device__ __forceinline__ void add_sample_f32(double* rep, int scol, int srow, 
 //    the image border (sift.cpp:634-656);
 //  * a wave scan of the row lengths, then sample t0 + lane is located by a
 //    branch-free binary search over the 64 inclusive prefixes;
-//  * the next step's four gradient loads per lane are in flight while the
-//    current step's samples are processed (issued unconditionally: lanes
-//    past the end read pixel (1, 1), so the compiler can count them).
+//  * the next SIFT_DESC_AHEAD steps' four gradient loads per lane are in
+//    flight while the current step's samples are processed (issued
+//    unconditionally: lanes past the end read pixel (1, 1), so the compiler
+//    can count them).
 // ---------------------------------------------------------------------------
 template <bool F64, int NR>
 __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, double* rep,
@@ -276,23 +280,35 @@ __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, d
             v[2] = img[r0 - W];
             v[3] = img[r0 + W];
         };
-        int srow = 0, scol = 0, nrow = 0, ncol = 0;
-        double cv[4], nv[4];
-        bool cok = total > 0 && locate(0, srow, scol);
-        fetch(cok, srow, scol, cv);
-        for (int t0 = 0; t0 < total; t0 += 64) {
-            nrow = ncol = 0;
-            const bool nok = t0 + 64 < total && locate(t0 + 64, nrow, ncol);
-            fetch(nok, nrow, ncol, nv);
-            if (cok) {
-                if (F64) add_sample_f64<NR>(rep, scol, srow, cv, d, atab, gtab);
-                else add_sample_f32<NR>(rep, scol, srow, cv, d);
-            }
-            srow = nrow;
-            scol = ncol;
-            cok = nok;
+        // a ring of AHEAD + 1 steps: step t0 is processed while the loads
+        // of the next AHEAD steps are in flight (slots are compile-time:
+        // the queue shifts by register moves)
+        constexpr int A = SIFT_DESC_AHEAD;
+        int qrow[A + 1], qcol[A + 1];
+        bool qok[A + 1];
+        double qv[A + 1][4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
+        for (int a = 0; a < A; ++a) {
+            qrow[a] = qcol[a] = 0;
+            qok[a] = 64 * a < total && locate(64 * a, qrow[a], qcol[a]);
+            fetch(qok[a], qrow[a], qcol[a], qv[a]);
+        }
+        for (int t0 = 0; t0 < total; t0 += 64) {
+            qrow[A] = qcol[A] = 0;
+            qok[A] = t0 + 64 * A < total && locate(t0 + 64 * A, qrow[A], qcol[A]);
+            fetch(qok[A], qrow[A], qcol[A], qv[A]);
+            if (qok[0]) {
+                if (F64) add_sample_f64<NR>(rep, qcol[0], qrow[0], qv[0], d, atab, gtab);
+                else add_sample_f32<NR>(rep, qcol[0], qrow[0], qv[0], d);
+            }
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                qrow[a] = qrow[a + 1];
+                qcol[a] = qcol[a + 1];
+                qok[a] = qok[a + 1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
+            }
         }
     }
 }
