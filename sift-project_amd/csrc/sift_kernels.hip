@@ -44,6 +44,9 @@
 #ifndef SIFT_PRIO_LDS
 #define SIFT_PRIO_LDS 1
 #endif
+#ifndef SIFT_ORI_AHEAD  // k_orient_wave: steps of 64 samples whose loads are in flight
+#define SIFT_ORI_AHEAD 1
+#endif
 #ifndef SIFT_ORI_FAST  // k_orient_wave: sqrt_f64 + atan2_f32 (0: ocml sqrt + atan2f, A/B)
 #define SIFT_ORI_FAST 1
 #endif
@@ -1215,13 +1218,29 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             v[3] = img[r0 + W];
             return ok;
         };
-        double cv[4], nv[4];
-        bool cok = fetch(lane, ci_, cj_, cv);
-        int ni_ = ci_, nj_ = cj_;
-        advance(ni_, nj_);
+        // a ring of A + 1 steps of 64 samples: step s0 is processed while
+        // the loads of the next A steps are in flight
+        constexpr int A = SIFT_ORI_AHEAD;
+        int qi[A + 1], qj[A + 1];
+        bool qok[A + 1];
+        double qv[A + 1][4];
+        int pi_ = ci_, pj_ = cj_;  // position of the next step to fetch
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            qi[a] = pi_;
+            qj[a] = pj_;
+            qok[a] = fetch(64 * a + lane, pi_, pj_, qv[a]);
+            advance(pi_, pj_);
+        }
         for (int s0 = 0; s0 < nsamp; s0 += 64) {
-            const bool nok = fetch(s0 + 64 + lane, ni_, nj_, nv);
-            if (cok) {
+            qi[A] = pi_;
+            qj[A] = pj_;
+            qok[A] = fetch(s0 + 64 * A + lane, pi_, pj_, qv[A]);
+            advance(pi_, pj_);
+            if (qok[0]) {
+                const double* cv = qv[0];
+                ci_ = qi[0];
+                cj_ = qj[0];
                 const double dx = cv[0] - cv[1];
                 const double dy = cv[2] - cv[3];
 #if SIFT_ORI_FAST
@@ -1242,11 +1261,13 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
                 atomicAdd(&rep[hidx * kOriWReps], wgt * mag);
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cv[q] = nv[q];
-            cok = nok;
-            ci_ = ni_;
-            cj_ = nj_;
-            advance(ni_, nj_);
+            for (int a = 0; a < A; ++a) {
+                qi[a] = qi[a + 1];
+                qj[a] = qj[a + 1];
+                qok[a] = qok[a + 1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
+            }
         }
         wave_sync();
         // smoothing (sift.cpp:496-504) and peaks (sift.cpp:507-531)
