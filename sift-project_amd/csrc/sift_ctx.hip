@@ -203,6 +203,7 @@ struct Slot {
     size_t ev_used = 0;
     unsigned uses = 0;  // mask of sift_ctx::pool streams this job runs on
     hipEvent_t done_ev = nullptr;  // lane counters on the host
+    hipEvent_t pyr0_ev = nullptr;  // octave 0 of this job's pyramid built (pyramid token)
     // streams of the current job: A, B pyramid (even / odd octaves), C, D
     // keypoint lanes 0 / 1 (A == B and C == D when the job runs alone on its
     // slot's pair)
@@ -291,6 +292,15 @@ struct sift_ctx {
     // bursts). Launch graphs per slot cut the host's enqueue from 0.12 to
     // 0.03 ms per job but ran the step 2 % slower (profiles/r03_j): removed.
     int pipe_hint = 0;
+    // Pyramid token (SIFT_PYR_CHAIN): a job's pyramid waits for the previous
+    // job's octave 0 (an event). In the steady state of a pipeline it is long
+    // built; a burst of jobs submitted together (a pipeline filling) would
+    // otherwise run their HBM-bound octave-0 blurs side by side and then
+    // their latency-bound keypoint chains side by side, instead of the
+    // staggered mix of the steady state, and the first job of the burst
+    // finishes late.
+    bool pyr_chain = true;
+    int pyr_last = -1;  // slot of the last job that recorded its token
     // SIFT_DESC_MODE: 0 = k_descriptor_split, f64 sample math (default, the
     // reference's arithmetic); A/B only: 1 = k_descriptor_wave (f32 sample
     // math, a wavefront per record), 2 = k_descriptor_split with f32 math
@@ -629,6 +639,12 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         return SIFT_OK;
     };
 
+    // ---- pyramid token: this job's pyramid starts once the previous job's
+    // octave 0 is built (sift_ctx::pyr_chain)
+    if (ctx->pyr_chain && ctx->pyr_last >= 0 && ctx->pyr_last != (int)(&s - ctx->slots) &&
+        ctx->slots[ctx->pyr_last].state == kSubmitted)
+        SIFT_HIP_TRY(hipStreamWaitEvent(sA, ctx->slots[ctx->pyr_last].pyr0_ev, 0));
+
     // ---- Gaussian pyramid (compute_initial_image + compute_gaussian_images)
     const int W0 = g.W[0], H0 = g.H[0];
     {
@@ -760,6 +776,10 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 if (!base_ready) return SIFT_ERR_HIP;
                 SIFT_HIP_TRY(hipEventRecord(base_ready, so));
             }
+        }
+        if (o == 0 && ctx->pyr_chain) {
+            SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, so));
+            ctx->pyr_last = (int)(&s - ctx->slots);
         }
         if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
     }
@@ -1194,6 +1214,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e) != 0;
     bool ok = prepare_kernel_attributes() == hipSuccess;
     ok = ok && hipMalloc(&ctx->d_done, sizeof(unsigned)) == hipSuccess &&
          hipMemset(ctx->d_done, 0, sizeof(unsigned)) == hipSuccess;
@@ -1215,7 +1236,8 @@ int sift_hip_create(int device, sift_ctx** out) {
              hipHostMalloc(&s.h_ctr, 4 * kLanes * sizeof(unsigned)) == hipSuccess &&
              hipHostMalloc(&s.h_stage, sizeof(Stage)) == hipSuccess &&
              hipMalloc(&s.d_stage, sizeof(Stage)) == hipSuccess &&
-             hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming) == hipSuccess;
+             hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&s.pyr0_ev, hipEventDisableTiming) == hipSuccess;
     }
     if (!ok) {
         sift_hip_destroy(ctx);
@@ -1262,6 +1284,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
         for (hipEvent_t e : s.sync_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : s.ev_pool) (void)hipEventDestroy(e);
         if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+        if (s.pyr0_ev) (void)hipEventDestroy(s.pyr0_ev);
     }
     if (ctx->d_mbuf) (void)hipFree(ctx->d_mbuf);
     ctx->h_mj.release();

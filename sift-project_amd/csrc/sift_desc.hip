@@ -27,7 +27,7 @@
 #define SIFT_DSPLIT_OCC (SIFT_DSPLIT_REPS >= 16 ? 2 : 3)
 #endif
 #ifndef SIFT_DESC_AHEAD  // steps of 64 samples whose gradient loads are in flight
-#define SIFT_DESC_AHEAD 2
+#define SIFT_DESC_AHEAD 1
 #endif
 #ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
 #define SIFT_DESCW_REPS 16
