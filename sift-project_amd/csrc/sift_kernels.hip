@@ -44,6 +44,12 @@
 #ifndef SIFT_PRIO_LDS
 #define SIFT_PRIO_LDS 1
 #endif
+#ifndef SIFT_BLUR_BIG_ROWS  // k_blur strip rows / columns per lane on planes >= 4 Mpx (A/B)
+#define SIFT_BLUR_BIG_ROWS 32
+#endif
+#ifndef SIFT_BLUR_BIG_COLS
+#define SIFT_BLUR_BIG_COLS 2
+#endif
 #ifndef SIFT_ORI_AHEAD  // k_orient_wave: steps of 64 samples whose loads are in flight
 #define SIFT_ORI_AHEAD 1
 #endif
@@ -1424,7 +1430,8 @@ BlurShape blur_shape_for(int W, int H, int R) {
     const size_t px = (size_t)W * H;
     BlurShape b;
     b.cols = (!(W & 1) && px >= ((size_t)1 << 20)) ? 2 : 1;
-    b.rows = px >= ((size_t)4 << 20) ? 32 : 16;  // 48 / 64 / 96 rows measured slower
+    if (px >= ((size_t)4 << 20)) b.cols = std::min(b.cols, SIFT_BLUR_BIG_COLS);
+    b.rows = px >= ((size_t)4 << 20) ? SIFT_BLUR_BIG_ROWS : 16;  // 48 / 64 / 96 rows measured slower
     if (R > 12 && b.cols == 2) b.rows = 16;
     if (b.rows > H) b.rows = H;
     return b;
