@@ -248,11 +248,15 @@ struct sift_ctx {
     // and memory bandwidth from the other jobs' blurs (round 3, interleaved
     // A/B on 1080p, single-image jobs four in flight: 192 per image 0.521
     // ms, 256 0.527, 512 0.548; 8-image jobs 0.503 ms per image at 512 in
-    // all vs 0.537 at 1024). A job alone on the chip gets the same grid:
-    // 1024 workgroups starved the concurrent small-octave blurs on its
-    // critical path. SIFT_KP_WGS / SIFT_DESC_WGS (tuning).
-    unsigned kp_wgs = 192;
-    unsigned desc_wgs = 384;  // k_descriptor_split: ONE record per workgroup
+    // all vs 0.537 at 1024). Round 4 with the f64 split descriptor (one
+    // record per workgroup): orientation 128 / descriptor 256 per image
+    // -1.1 % against 192 / 384 (512 descriptor workgroups +1.3 %, 384
+    // orientation workgroups +3.8 %). A job alone on the chip gets the same
+    // grid (1024 workgroups starved the concurrent small-octave blurs on its
+    // critical path) except for its last chain (enqueue_chain). SIFT_KP_WGS /
+    // SIFT_DESC_WGS (tuning).
+    unsigned kp_wgs = 128;
+    unsigned desc_wgs = 256;  // k_descriptor_split: ONE record per workgroup
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
     // rest form one final batch after the LDS octaves. A single-image job
     // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
@@ -300,6 +304,11 @@ struct sift_ctx {
     // staggered mix of the steady state, and the first job of the burst
     // finishes late.
     bool pyr_chain = true;
+    // SIFT_LEAD_ALONE: a job submitted when none is in flight takes all four
+    // pair streams (two keypoint lanes) even in a pipelining caller, so the
+    // first job of a burst finishes at its alone latency; the jobs behind it
+    // take the other streams of the pool
+    bool lead_alone = false;
     int pyr_last = -1;  // slot of the last job that recorded its token
     // SIFT_DESC_MODE: 0 = k_descriptor_split, f64 sample math (default, the
     // reference's arithmetic); A/B only: 1 = k_descriptor_wave (f32 sample
@@ -1072,7 +1081,7 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
         const bool hinted = ctx->pipe_hint > 0;
         if (others > 0) ctx->pipe_hint = kPipeHint;
         else if (ctx->pipe_hint > 0) --ctx->pipe_hint;
-        if (hinted || others > 0) {
+        if (others > 0 || (hinted && !ctx->lead_alone)) {
             int k = 0;
             while (k + 1 < kSlots && (used >> k & 1u)) ++k;
             s.sA = s.sB = s.sC = s.sD = q[k];
@@ -1215,6 +1224,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_LEAD_ALONE")) ctx->lead_alone = std::atoi(e) != 0;
     bool ok = prepare_kernel_attributes() == hipSuccess;
     ok = ok && hipMalloc(&ctx->d_done, sizeof(unsigned)) == hipSuccess &&
          hipMemset(ctx->d_done, 0, sizeof(unsigned)) == hipSuccess;
