@@ -54,6 +54,7 @@ namespace {
 using clk = std::chrono::steady_clock;
 
 constexpr unsigned kKpWgsMax = 512;               // keypoint workgroups per launch, at most
+constexpr unsigned kDescWgsAlone = 768;           // k_descriptor_split: 3 per CU resident
 constexpr size_t kTileMaxPx = (size_t)1 << 21;    // planes up to this size: LDS-tile blur
 
 // Keypoint lanes: batches alternate between two streams (C, D), each with
@@ -303,7 +304,9 @@ struct sift_ctx {
     // their latency-bound keypoint chains side by side, instead of the
     // staggered mix of the steady state, and the first job of the burst
     // finishes late.
-    bool pyr_chain = true;
+    long ext_waves = 512;   // SIFT_EXT_WAVES: extrema tasks per octave (extrema_grid)
+    int ext_seg_max = 32;   // SIFT_EXT_SEGMAX: centre rows per extrema task, at most
+    int pyr_chain = 1;  // 0 off; A/B: 2, 3 record the token later (enqueue_job)
     // SIFT_LEAD_ALONE: a job submitted when none is in flight takes all four
     // pair streams (two keypoint lanes) even in a pipelining caller, so the
     // first job of a burst finishes at its alone latency; the jobs behind it
@@ -399,17 +402,21 @@ int prof_events(sift_ctx* ctx, Slot& s, hipEvent_t* e0, hipEvent_t* e1, double b
 
 // task table of one k_extrema_stream launch over octaves [o_begin, o_end):
 // strips of kExtSpan centre columns x segments of centre rows
-ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img) {
+ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img, long waves,
+                         int seg_max) {
     ExtremaGrid eg;
     std::memset(&eg, 0, sizeof eg);
     for (int o = o_begin; o < o_end; ++o) {
         const int i = eg.n++;
         const int tx = g.W[o] > 2 ? (g.W[o] - 2 + kExtSpan - 1) / kExtSpan : 0;
-        // segments short enough for ~4096 waves per octave over the job (the
-        // small octaves are latency-bound; 3072 / 6144 / 12288 measured
-        // within 1 %), at least 4 rows (2 priming rows per segment), at most 64
-        const long rows = (long)tx * std::max(g.H[o] - 2, 0) * n_img / 4096L;
-        const int ch = (int)std::min<long>(64, std::max<long>(4, rows));
+        // segments for ~ext_waves waves per octave over the job, at least 4
+        // rows (2 priming rows per segment), at most ext_seg_max. Round 4
+        // (1080p): 512 waves / 32 rows: extrema alone 176 -> 135 us per image
+        // (octave 1 in 32-row instead of 8-row tasks), the driver's 20-step
+        // bench -3.5 %; 4096 / 64 was round 3's (3072 / 6144 / 12288 within
+        // 1 % there); 256 / 128 and 128 / 256 slower (too few waves)
+        const long rows = (long)tx * std::max(g.H[o] - 2, 0) * n_img / waves;
+        const int ch = (int)std::min<long>(seg_max, std::max<long>(4, rows));
         const int ty = g.H[o] > 2 ? (g.H[o] - 2 + ch - 1) / ch : 0;
         eg.oct[i] = o;
         eg.tiles_x[i] = tx > 0 ? tx : 1;
@@ -420,10 +427,10 @@ ExtremaGrid extrema_grid(const Geometry& g, int o_begin, int o_end, int n_img) {
 }
 
 hipError_t launch_extrema_set(const PyrTable* d_pt, const Geometry& g, int o_begin, int o_end,
-                              int n_img, int thr, sift_extremum* cand, unsigned* counter,
+                              int n_img, long waves, int seg_max, int thr, sift_extremum* cand, unsigned* counter,
                               unsigned cap, unsigned* snap, hipStream_t s, hipEvent_t e0,
                               hipEvent_t e1) {
-    const ExtremaGrid eg = extrema_grid(g, o_begin, o_end, n_img);
+    const ExtremaGrid eg = extrema_grid(g, o_begin, o_end, n_img, waves, seg_max);
     return launch_extrema_stream(d_pt, eg, n_img, g.n_gauss, thr, cand, counter, cap, snap, s, e0,
                                  e1);
 }
@@ -497,7 +504,8 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
         hipEvent_t e0, e1;
         if (prof_events(ctx, s, &e0, &e1, xb * n_img, SIFT_PROF_EXTREMA) != SIFT_OK)
             return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(launch_extrema_set(d_pt, g, o_begin, o_end, n_img, dp.threshold, cand,
+        SIFT_HIP_TRY(launch_extrema_set(d_pt, g, o_begin, o_end, n_img, ctx->ext_waves,
+                                        ctx->ext_seg_max, dp.threshold, cand,
                                         live + 0, cap_cand, begin, sx, e0, e1));
     } else {
         for (int o = o_begin; o < o_end; ++o)
@@ -507,13 +515,20 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
         if (begin) SIFT_HIP_TRY(launch_snapshot(live, begin, sx, 0, 3));
     }
     const unsigned* b = begin ? begin : zeros;
-    // persistent grid of this chain: kp_wgs / desc_wgs per image. The last
-    // chain of a job alone on the chip (two keypoint lanes) runs after its
-    // whole pyramid, with no blur left to starve: it takes kKpWgsMax
-    const bool tail = s.lanes > 1 && o_end == g.octaves;
-    const unsigned ori_wgs = tail ? kKpWgsMax : std::min(kKpWgsMax, ctx->kp_wgs * (unsigned)n_img);
+    // persistent grid of this chain: kp_wgs / desc_wgs per image while other
+    // jobs share the chip. Nothing else runs beside the last chain of a job
+    // alone on the chip (two keypoint lanes, after its whole pyramid) or a
+    // chain of a serialised context: those fill the chip (kKpWgsMax
+    // orientation workgroups, kDescWgsAlone one-record descriptor
+    // workgroups = every resident slot). The other chains of a job alone
+    // overlap its own smaller octaves' blurs: 1.5x the shared grid
+    const bool alone = ctx->serial || (s.lanes > 1 && o_end == g.octaves);
+    const unsigned scale2 = s.lanes > 1 ? 3u : 2u;  // x1.5 for a job alone, in halves
+    const unsigned ori_wgs =
+        alone ? kKpWgsMax : std::min(kKpWgsMax, ctx->kp_wgs * scale2 / 2u * (unsigned)n_img);
     const unsigned desc_wgs =
-        tail ? kKpWgsMax : std::min(kKpWgsMax, ctx->desc_wgs * (unsigned)n_img);
+        alone ? kDescWgsAlone
+              : std::min(kKpWgsMax, ctx->desc_wgs * scale2 / 2u * (unsigned)n_img);
     hipEvent_t r0, r1, q0, q1, d0, d1;  // profiling events of the keypoint stages
     if (prof_events(ctx, s, &r0, &r1, 0.0, SIFT_PROF_REFINE) != SIFT_OK ||
         prof_events(ctx, s, &q0, &q1, 0.0, SIFT_PROF_ORIENT) != SIFT_OK ||
@@ -786,11 +801,19 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 SIFT_HIP_TRY(hipEventRecord(base_ready, so));
             }
         }
-        if (o == 0 && ctx->pyr_chain) {
+        if (o == 0 && ctx->pyr_chain == 1) {
             SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, so));
             ctx->pyr_last = (int)(&s - ctx->slots);
         }
         if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
+        if (o == 0 && ctx->pyr_chain == 2) {  // A/B: token after octave 0's keypoints
+            SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, lane_stream[0]));
+            ctx->pyr_last = (int)(&s - ctx->slots);
+        }
+    }
+    if (ctx->pyr_chain == 3) {  // A/B: token after the pyramid's strip-walk octaves
+        SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, pyr[(o_small - 1) & 1]));
+        ctx->pyr_last = (int)(&s - ctx->slots);
     }
     if (o_small < g.octaves) {
         hipStream_t so = pyr[o_small & 1];
@@ -1223,7 +1246,9 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_EXT_WAVES")) ctx->ext_waves = std::max(64L, std::atol(e));
+    if (const char* e = std::getenv("SIFT_EXT_SEGMAX")) ctx->ext_seg_max = std::max(4, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e);
     if (const char* e = std::getenv("SIFT_LEAD_ALONE")) ctx->lead_alone = std::atoi(e) != 0;
     bool ok = prepare_kernel_attributes() == hipSuccess;
     ok = ok && hipMalloc(&ctx->d_done, sizeof(unsigned)) == hipSuccess &&

@@ -1431,7 +1431,8 @@ BlurShape blur_shape_for(int W, int H, int R) {
     BlurShape b;
     b.cols = (!(W & 1) && px >= ((size_t)1 << 20)) ? 2 : 1;
     if (px >= ((size_t)4 << 20)) b.cols = std::min(b.cols, SIFT_BLUR_BIG_COLS);
-    b.rows = px >= ((size_t)4 << 20) ? SIFT_BLUR_BIG_ROWS : 16;  // 48 / 64 / 96 rows measured slower
+    b.rows = px >= ((size_t)4 << 20) ? SIFT_BLUR_BIG_ROWS : 16;  // 48 / 64 / 96 rows measured slower;
+    // round 4: 24 / 48 / 64 rows for R >= 6 only: octave 0 alone within 1 %
     if (R > 12 && b.cols == 2) b.rows = 16;
     if (b.rows > H) b.rows = H;
     return b;

@@ -17,7 +17,7 @@ for r in $(seq 1 $N); do
     envs=""
     [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
     env $envs timeout -k 10 120 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
-        --no-matcher --no-alone --no-desc-f64 --no-extra > $O/v${i}_r$r.json 2> $O/v${i}_r$r.err \
+        --no-matcher --no-alone --no-big --no-extra > $O/v${i}_r$r.json 2> $O/v${i}_r$r.err \
         || { tail -5 $O/v${i}_r$r.err; exit 1; }
   done
 done

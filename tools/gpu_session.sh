@@ -33,7 +33,7 @@ for step in "$@"; do
         || { tail -20 $R/$O/bench_prof.err; exit 1; }
     SIFT_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $R/$O/ser -o run \
         -- python3 $R/bench.py --sync --steps 200 --warmup 10 --no-cpu-baseline --no-extra --no-matcher \
-        --no-alone --no-desc-f64 > $R/$O/bench_ser.json 2> $R/$O/bench_ser.err \
+        --no-alone --no-big > $R/$O/bench_ser.json 2> $R/$O/bench_ser.err \
         || { tail -20 $R/$O/bench_ser.err; exit 1; }
     cd $R
     python tools/prof_summary.py $O/prof/run_kernel_trace.csv > $O/summary.txt
@@ -55,7 +55,7 @@ for step in "$@"; do
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/$O/lat -o run \
         -- python3 $R/bench.py --sync --steps 100 --warmup 10 --no-cpu-baseline --no-extra \
-        --no-matcher --no-alone --no-desc-f64 --no-events > $R/$O/bench_lat.json 2> $R/$O/bench_lat.err \
+        --no-matcher --no-alone --no-big --no-events > $R/$O/bench_lat.json 2> $R/$O/bench_lat.err \
         || { tail -20 $R/$O/bench_lat.err; exit 1; }
     cd $R
     python tools/prof_summary.py $O/lat/run_kernel_trace.csv > $O/summary_lat.txt
@@ -64,7 +64,7 @@ for step in "$@"; do
   steplog)
     # the driver's bench shape with the timed region's submit / fetch / done times
     timeout -k 10 120 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-matcher \
-        --no-alone --no-desc-f64 --no-extra --step-log > $O/steplog.json 2> $O/steplog.err \
+        --no-alone --no-big --no-extra --step-log > $O/steplog.json 2> $O/steplog.err \
         || { tail -20 $O/steplog.err; exit 1; }
     grep -A70 "step log" $O/steplog.err ;;
   divcheck)

@@ -13,6 +13,6 @@ P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BA
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  SIFT_SERIAL=1 timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex 'k_descriptor|k_orient|k_refine|k_extrema|k_blur|k_octaves' --output-format csv -d $O/pass$i -o run -- python3 $R/bench.py --steps 5 --warmup 2 --sync --no-extra --no-cpu-baseline --no-matcher --no-events --no-alone --no-desc-f64 > $O/pass$i.log 2>&1 || { tail -5 $O/pass$i.log; exit 1; }
+  SIFT_SERIAL=1 timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex 'k_descriptor|k_orient|k_refine|k_extrema|k_blur|k_octaves' --output-format csv -d $O/pass$i -o run -- python3 $R/bench.py --steps 5 --warmup 2 --sync --no-extra --no-cpu-baseline --no-matcher --no-events --no-alone --no-big > $O/pass$i.log 2>&1 || { tail -5 $O/pass$i.log; exit 1; }
 done
 echo PMC_DONE

@@ -11,6 +11,6 @@ mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/calib_$C -o run -- $R/tools/pmc_calib > $O/calib_$C.log 2>&1 || exit 1
-  timeout -s KILL 200 rocprofv3 --pmc $C --kernel-include-regex 'k_blur|k_octaves_lds|k_extrema' --output-format csv -d $O/bench_$C -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-extra --no-cpu-baseline --no-matcher --no-alone > $O/bench_$C.log 2>&1 || exit 1
+  timeout -s KILL 200 rocprofv3 --pmc $C --kernel-include-regex 'k_blur|k_octaves_lds|k_extrema' --output-format csv -d $O/bench_$C -o run -- python3 $R/bench.py --steps 20 --warmup 2 --no-extra --no-cpu-baseline --no-matcher --no-alone --no-big > $O/bench_$C.log 2>&1 || exit 1
 done
 echo PMC_DONE

@@ -22,6 +22,16 @@ def main(path, n_images=None):
     print(f"{'kernel':40s} {'calls':>6s} {'total us':>10s} {'avg us':>9s} {'us/image':>9s}")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"{k[:40]:40s} {cnt[k]:6d} {v:10.1f} {v / cnt[k]:9.2f} {v / n_img:9.1f}")
+    # kernel families as bench.py's roofline / keypoint_kernels_alone rows
+    fams = {"pyramid": ("k_blur", "k_blur_tile", "k_octaves_lds"), "extrema": ("k_extrema",),
+            "refine": ("k_refine",), "orientation": ("k_orient",), "descriptor": ("k_descriptor",)}
+    print(f"\n{'family':12s} {'launches':>9s} {'us/image':>9s} {'avg us/launch':>14s}")
+    for f, pre in fams.items():
+        ks = [k for k in tot if k.split("(")[0] in pre or
+              (f != "pyramid" and any(k.startswith(p) for p in pre))]
+        t, c = sum(tot[k] for k in ks), sum(cnt[k] for k in ks)
+        if c:
+            print(f"{f:12s} {c:9d} {t / n_img:9.1f} {t / c:14.2f}")
     if len(starts) >= 2:
         a, b = starts[-2], starts[-1]
         # the image's first pyramid launch precedes its memset by a few dispatches
