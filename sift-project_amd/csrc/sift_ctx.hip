@@ -537,7 +537,7 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
                                raw, live + 1, cap_raw, sx, r0, r1));
     SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
-                               cap_ori, work, ori_wgs, sx, q0, q1));
+                               cap_ori, work, ori_wgs, alone, sx, q0, q1));
     SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
                                    work + 2, c.ex, desc_wgs, ctx->desc_mode, sx, d0, d1));
     return SIFT_OK;

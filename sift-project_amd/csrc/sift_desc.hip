@@ -371,7 +371,7 @@ __device__ __forceinline__ void finish_record(double v0, double v1, const DescRe
 
 // ---------------------------------------------------------------------------
 // k_descriptor_split<F64> (desc_mode 0 with F64, the default): one record
-// per 256-thread workgroup, from the work counter.
+// per 256-thread workgroup.
 //  * Row j of the window goes to wave j % 4 (desc_walk with dj = 4), so a
 //    record takes a quarter of a wavefront's serial walk, and the split
 //    depends only on the record: its bytes do not depend on how its job
@@ -382,9 +382,10 @@ __device__ __forceinline__ void finish_record(double v0, double v1, const DescRe
 //    reduces its replicas to two bins per lane, wave 0 sums the four waves'
 //    partials in wave order and finishes the record. Fixed order
 //    throughout: the bytes depend only on the record.
-//  * One lane of wave 1 claims the next record (and evaluates the f64
-//    sin / cos of its orientation, once per record) while wave 0 finishes
-//    the current one; two barriers per record.
+//  * Workgroup b's first record is b; one lane of wave 1 claims the next
+//    (work counter) and evaluates the f64 sin / cos of its orientation (once
+//    per record) while wave 0 finishes the current one; two barriers per
+//    record.
 // ---------------------------------------------------------------------------
 constexpr int kSplitReps = SIFT_DSPLIT_REPS;
 // Gaussian weight table G(0..radius) of the current record (split kernel,
@@ -419,18 +420,22 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
         ex.cnt[1] = n;
     }
     if (threadIdx.x < 17) atab[threadIdx.x] = kAtanTab[threadIdx.x];
-    auto claim_next = [&]() {
-        const unsigned c = atomicAdd(work, 1u);
+    // workgroup b's first record is b of the launch's range, the later ones
+    // come from the work counter offset by the grid (every workgroup claiming
+    // at once at the start serialised at one L2 channel, ~10 ns per atomic;
+    // static striding throughout measured slower: no dynamic balance)
+    auto prepare = [&](unsigned c) {
         next_k = c;
         if (F64 && k0 + c < n) {
             const double pr = recs[k0 + c].pori;
             next_sc = make_double2(sin(pr), cos(pr));
         }
     };
-    if (threadIdx.x == 0) claim_next();
+    if (threadIdx.x == 0) prepare(blockIdx.x);
     __syncthreads();
     for (;;) {
-        const unsigned k = k0 + next_k;
+        const unsigned cur = next_k;
+        const unsigned k = k0 + cur;
         if (k >= n) break;
         const double2 sc = next_sc;
         const DescRecord d = load_record<F64>(pt, P, recs[k], rec_side[k], &sc);
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
             }
             finish_record(v0, v1, d, k, recs, desc_f32, ex);
         } else if (wv == 1 && lane == 0) {
-            claim_next();
+            prepare(gridDim.x + atomicAdd(work, 1u));
         }
         __syncthreads();
     }
@@ -467,11 +472,11 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
 
 // ---------------------------------------------------------------------------
 // k_descriptor_wave<F64> (A/B: desc_mode 1 f32, 3 f64): one WAVEFRONT per
-// record, four independent waves per workgroup pulling records from the work
-// counter; no workgroup barrier anywhere (a wave's LDS instructions execute
-// in order, so zeroing -> accumulation -> reduction -> next record's zeroing
-// needs only compiler ordering, wave_sync). A record's samples are one
-// wave's serial walk.
+// record, four independent waves per workgroup (wave g's first record is g,
+// then the work counter); no workgroup barrier anywhere (a
+// wave's LDS instructions execute in order, so zeroing -> accumulation ->
+// reduction -> next record's zeroing needs only compiler ordering,
+// wave_sync). A record's samples are one wave's serial walk.
 // ---------------------------------------------------------------------------
 constexpr int kDescWReps = SIFT_DESCW_REPS;
 static_assert(kDescWReps >= 1 && kDescWReps <= 16 && (kDescWReps & (kDescWReps - 1)) == 0,
@@ -500,11 +505,8 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
         if (threadIdx.x < 17) atab[threadIdx.x] = kAtanTab[threadIdx.x];
         __syncthreads();  // the only barrier, before any wave can leave
     }
-    for (;;) {
-        unsigned claim = 0;
-        if (lane == 0) claim = atomicAdd(work, 1u);
-        const unsigned k = k0 + __builtin_amdgcn_readfirstlane(claim);
-        if (k >= n) break;
+    const unsigned n_waves = gridDim.x * 4;
+    for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n;) {  // first static, as split
         const DescRecord d = load_record<F64>(pt, P, recs[k], rec_side[k], nullptr);
         for (int i = lane; i < 64 * kDescWReps; i += 64)
             reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
@@ -515,6 +517,9 @@ __global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
         reduce_replicas<kDescWReps>(hist, v0, v1);
         finish_record(v0, v1, d, k, recs, desc_f32, ex);
         wave_sync();
+        unsigned claim = 0;
+        if (lane == 0) claim = atomicAdd(work, 1u);
+        k = k0 + n_waves + __builtin_amdgcn_readfirstlane(claim);
     }
 }
 

@@ -69,7 +69,7 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
-                         unsigned* work, unsigned wgs, hipStream_t s,
+                         unsigned* work, unsigned wgs, bool static_walk, hipStream_t s,
                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
                              const RecSide* rec_side, const unsigned* rec_begin,

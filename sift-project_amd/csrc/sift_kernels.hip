@@ -53,6 +53,12 @@
 #ifndef SIFT_ORI_AHEAD  // k_orient_wave: steps of 64 samples whose loads are in flight
 #define SIFT_ORI_AHEAD 1
 #endif
+// SIFT_LAB_ORI: attribution builds only (make alt; wrong results): 1 no
+// histogram atomics, 2 no sqrt / atan2, 3 no smoothing, 4 no window sweep,
+// 5 claims only, 6 no sweep and no weight table
+#ifndef SIFT_LAB_ORI
+#define SIFT_LAB_ORI 0
+#endif
 #ifndef SIFT_ORI_FAST  // k_orient_wave: sqrt_f64 + atan2_f32 (0: ocml sqrt + atan2f, A/B)
 #define SIFT_ORI_FAST 1
 #endif
@@ -1157,15 +1163,19 @@ constexpr int kOriWTab = SIFT_ORIW_TAB;
 #endif
 constexpr int kOriWReps = SIFT_ORIW_REPS;
 
+// records a wave buffers (keypoint index, orientation) before one counter
+// atomic appends them: the peaks of every keypoint a wave handles
+constexpr int kOriEmit = 64;
+
 __host__ __device__ constexpr int ori_wave_lds_doubles(int nb) {
-    return kOriWReps * nb + kOriWTab + (nb > 64 ? nb : 0);
+    return kOriWReps * nb + kOriWTab + (nb > 64 ? nb : 0) + 2 * kOriEmit;
 }
 
 __global__ __launch_bounds__(256, 4) void k_orient_wave(
     const PyrTable* __restrict__ pt, DevParams P, const RawKp* __restrict__ raw,
     const unsigned* __restrict__ raw_begin, const unsigned* __restrict__ n_raw, unsigned cap_raw,
     sift_kp* __restrict__ recs, RecSide* __restrict__ rec_side, unsigned* __restrict__ n_rec,
-    unsigned cap_rec, unsigned* __restrict__ work) {
+    unsigned cap_rec, unsigned* __restrict__ work, bool static_walk) {
     extern __shared__ double ori_wdyn[];
     set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;
@@ -1177,13 +1187,54 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
     double* const rep = hist + (lane & (kOriWReps - 1));  // bin b at rep[b * kOriWReps]
     double* const wtab = hist + kOriWReps * nb;
     double* const hs = wtab + kOriWTab;  // num_bins > 64 only
+    double* const eori = hs + (nb > 64 ? nb : 0);                   // buffered records:
+    unsigned* const ekp = reinterpret_cast<unsigned*>(eori + kOriEmit);  // orientation, keypoint
     const double bin_guard = nb * 3e-6;  // f32 bin error bound x 10 (see above)
     const float nbf = (float)nb;
-    for (;;) {
-        unsigned claim = 0;
-        if (lane == 0) claim = atomicAdd(work, 1u);
-        const unsigned k = k0 + __builtin_amdgcn_readfirstlane(claim);
-        if (k >= n) break;
+    unsigned nbuf = 0;  // wave-uniform
+    // the buffered records go out with one counter atomic; a record's fields
+    // come from its keypoint (sift.cpp:515-528)
+    auto flush = [&]() {
+        if (nbuf == 0) return;
+        wave_sync();
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(n_rec, nbuf);
+        base = __builtin_amdgcn_readfirstlane(base);
+        for (unsigned i = lane; i < nbuf; i += 64) {
+            const unsigned rec = base + i;
+            if (rec >= cap_rec) continue;
+            const RawKp q = raw[ekp[i]];
+            double rx = q.x, ry = q.y, rs = q.size;
+            if (P.double_image) {  // sift.cpp:522-526
+                rx /= 2;
+                ry /= 2;
+                rs /= 2;
+            }
+            sift_kp& r = recs[rec];
+            r.x = rx;
+            r.y = ry;
+            r.octave = q.octave;
+            r.layer = q.layer;
+            r.size = rs;
+            r.pori = eori[i];
+            rec_side[rec] = RecSide{q.off0, q.img, 0};
+        }
+        wave_sync();
+        nbuf = 0;
+    };
+    // wave g's first keypoint is g of the launch's range, the later ones come
+    // from the work counter (offset by the grid's waves): same-address
+    // atomics serialise at one L2 channel (~10 ns each), and every wave
+    // claiming at once at the start cost the last one ~20 us. static_walk
+    // (a launch alone on the chip, ~2 keypoints per wave): g, g + waves, ...
+    // with no counter at all (1080p alone 92 -> 75 us; sharing the chip with
+    // fewer waves, ~9 keypoints each, the dynamic balance wins by 1 %)
+    const unsigned n_waves = gridDim.x * 4;
+    for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n;) {
+        if (SIFT_LAB_ORI == 5) {
+            k = n;
+            continue;
+        }
         const RawKp kp = raw[k];
         const int o = kp.octave;
         const double inv = 1.0 / pow2i(o);
@@ -1198,7 +1249,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
         const int kmax = 2 * radius * radius;
         const bool use_tab = kmax < kOriWTab;
         for (int i = lane; i < kOriWReps * nb; i += 64) hist[i] = 0.0;
-        if (use_tab)
+        if (use_tab && SIFT_LAB_ORI != 6)
             for (int q = lane; q <= kmax; q += 64) wtab[q] = exp(-q / denom);
         wave_sync();
         // the side x side window flattened, 64 samples per step; sample s
@@ -1238,7 +1289,9 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             qok[a] = fetch(64 * a + lane, pi_, pj_, qv[a]);
             advance(pi_, pj_);
         }
-        for (int s0 = 0; s0 < nsamp; s0 += 64) {
+        double lab_acc = 0.0;  // SIFT_LAB_ORI attribution builds only
+        (void)lab_acc;
+        for (int s0 = 0; s0 < (SIFT_LAB_ORI >= 4 ? 0 : nsamp); s0 += 64) {
             qi[A] = pi_;
             qj[A] = pj_;
             qok[A] = fetch(s0 + 64 * A + lane, pi_, pj_, qv[A]);
@@ -1249,7 +1302,10 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
                 cj_ = qj[0];
                 const double dx = cv[0] - cv[1];
                 const double dy = cv[2] - cv[3];
-#if SIFT_ORI_FAST
+#if SIFT_LAB_ORI == 2
+                const double mag = dx * dx + dy * dy;
+                const float at = (float)dx;
+#elif SIFT_ORI_FAST
                 const double mag = sqrt_f64(dx * dx + dy * dy);  // correctly rounded
                 const float at = atan2_f32((float)dy, (float)dx);
 #else
@@ -1264,7 +1320,11 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
                 if (fabs((double)t - floor((double)t) - 0.5) < bin_guard || tiny)
                     hidx = (int)round(nb * (atan2(dy, dx) + kPi) / kTwoPi);  // exact path
                 hidx = (hidx < nb) ? hidx : 0;
+#if SIFT_LAB_ORI == 1
+                lab_acc += wgt * mag + hidx;
+#else
                 atomicAdd(&rep[hidx * kOriWReps], wgt * mag);
+#endif
             }
 #pragma unroll
             for (int a = 0; a < A; ++a) {
@@ -1275,31 +1335,22 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
                 for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
             }
         }
+#if SIFT_LAB_ORI == 1
+        if (lab_acc == 1234.5) hist[lane] = lab_acc;
+#endif
         wave_sync();
         // smoothing (sift.cpp:496-504) and peaks (sift.cpp:507-531)
-        double rx = kp.x, ry = kp.y, rs = kp.size;
-        if (P.double_image) {  // sift.cpp:522-526
-            rx /= 2;
-            ry /= 2;
-            rs /= 2;
-        }
-        auto emit = [&](bool peak, double ori) {  // one counter atomic per wave
+        auto emit = [&](bool peak, double ori) {  // into the wave's buffer
             const unsigned long long m = __ballot(peak);
             if (!m) return;
-            unsigned base = 0;
-            if (lane == 0) base = atomicAdd(n_rec, (unsigned)__popcll(m));
-            base = __builtin_amdgcn_readfirstlane(base);
-            const unsigned rec = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-            if (peak && rec < cap_rec) {
-                sift_kp& r = recs[rec];
-                r.x = rx;
-                r.y = ry;
-                r.octave = kp.octave;
-                r.layer = kp.layer;
-                r.size = rs;
-                r.pori = ori;
-                rec_side[rec] = RecSide{kp.off0, kp.img, 0};
+            const unsigned c = (unsigned)__popcll(m);  // <= 64 = kOriEmit
+            if (nbuf + c > kOriEmit) flush();
+            if (peak) {
+                const unsigned i = nbuf + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                eori[i] = ori;
+                ekp[i] = k;
             }
+            nbuf += c;
         };
         auto interp = [&](int i, double h0, double h1, double h2) {
             double fi = i + 0.5 * (h0 - h2) / (h0 - 2 * h1 + h2);
@@ -1315,7 +1366,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
 #pragma unroll
                 for (int q = 0; q < kOriWReps; ++q)
                     h += hist[lane * kOriWReps + ((q + lane) & (kOriWReps - 1))];
-            for (int it = 0; it < kSmoothIters; ++it) {
+            for (int it = 0; it < (SIFT_LAB_ORI == 3 ? 0 : kSmoothIters); ++it) {
                 const double hn = __shfl(h, lane + 1 < nb ? lane + 1 : 0);  // old h[i+1]
                 const double c = 0.5 * h, d = 0.25 * hn;
                 double prev = readlane_f64(h, nb - 1);  // h[i-1] for i = 0: old
@@ -1380,7 +1431,15 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             }
         }
         wave_sync();
+        if (static_walk) {
+            k += n_waves;
+        } else {
+            unsigned claim = 0;
+            if (lane == 0) claim = atomicAdd(work, 1u);
+            k = k0 + n_waves + __builtin_amdgcn_readfirstlane(claim);
+        }
     }
+    flush();
 }
 
 // ---------------------------------------------------------------------------
@@ -1749,13 +1808,14 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,
                          const unsigned* raw_begin, const unsigned* n_raw, unsigned cap_raw,
                          sift_kp* recs, RecSide* rec_side, unsigned* n_rec, unsigned cap_rec,
-                         unsigned* work, unsigned wgs, hipStream_t s, hipEvent_t e0,
-                         hipEvent_t e1) {
+                         unsigned* work, unsigned wgs, bool static_walk, hipStream_t s,
+                         hipEvent_t e0, hipEvent_t e1) {
     // persistent: four waves per workgroup, a keypoint per wave
     const unsigned blocks = std::min<unsigned>(wgs, cap_raw > 0 ? (cap_raw + 3) / 4 : 1);
     const size_t lds = (size_t)4 * ori_wave_lds_doubles(P.num_bins) * sizeof(double);
     return launch_timed(k_orient_wave, dim3(blocks), dim3(256), lds, s, e0, e1, d_pt, P, raw,
-                        raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work);
+                        raw_begin, n_raw, cap_raw, recs, rec_side, n_rec, cap_rec, work,
+                        static_walk);
 }
 
 }  // namespace sift_amd
