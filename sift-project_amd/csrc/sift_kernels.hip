@@ -813,9 +813,13 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
     constexpr int PF = SIFT_EXT_PF;  // rows in flight
     constexpr unsigned kCandBuf = 256;  // per-wave candidate buffer (LDS)
     __shared__ sift_extremum cbuf[4][kCandBuf];
+    __shared__ unsigned wg_n[4], wg_base[4];
     const int lane = threadIdx.x & 63;
-    const int task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int wv = threadIdx.x >> 6;
+    const int task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
     const int b = blockIdx.y;
+    sift_extremum* cb = cbuf[wv];
+    unsigned nbuf = 0;  // wave-uniform
     if (task < eg.first_tile[eg.n]) {
         int e = 0;
         while (e + 1 < eg.n && task >= eg.first_tile[e + 1]) ++e;
@@ -835,12 +839,13 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
         for (int l = 0; l < NL; ++l) lv[l] = gbl(plane(pt, b, o, l)) + gx;
         const double dthr = (double)thr;
         const int otag = o | (b << kOctBits);
-        // candidates collect in a per-wave LDS buffer and go out with ONE
-        // counter atomic per wave (per full buffer): a returning atomic per
-        // (row, layer) on the single global counter serialised the whole
-        // launch on the small octaves, where candidates are dense
-        sift_extremum* cb = cbuf[threadIdx.x >> 6];
-        unsigned nbuf = 0;  // wave-uniform
+        // candidates collect in a per-wave LDS buffer; a full buffer goes out
+        // with one counter atomic, the rest with ONE atomic per workgroup at
+        // the end: a returning atomic per (row, layer) on the single global
+        // counter serialised the whole launch on the small octaves, where
+        // candidates are dense, and same-address atomics serialise at one
+        // L2 channel (~10 ns each: one per wave was ~40 us of a 1080p
+        // octave-0 launch's ~4200 waves)
         auto flush = [&]() {
             if (nbuf == 0) return;
             wave_sync();
@@ -924,8 +929,22 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
                 }
             }
         }
-        flush();
     }
+    // the workgroup's remaining candidates: one counter atomic
+    if (lane == 0) wg_n[wv] = nbuf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = wg_n[0] + wg_n[1] + wg_n[2] + wg_n[3];
+        const unsigned base = t ? atomicAdd(counter, t) : 0u;
+        wg_base[0] = base;
+        wg_base[1] = base + wg_n[0];
+        wg_base[2] = wg_base[1] + wg_n[1];
+        wg_base[3] = wg_base[2] + wg_n[2];
+    }
+    __syncthreads();
+    const unsigned base = wg_base[wv];
+    for (unsigned i = lane; i < nbuf; i += 64)
+        if (base + i < cap) out[base + i] = cb[i];
     snapshot_if_last(snap, counter);
 }
 
@@ -1192,14 +1211,9 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
     const double bin_guard = nb * 3e-6;  // f32 bin error bound x 10 (see above)
     const float nbf = (float)nb;
     unsigned nbuf = 0;  // wave-uniform
-    // the buffered records go out with one counter atomic; a record's fields
-    // come from its keypoint (sift.cpp:515-528)
-    auto flush = [&]() {
-        if (nbuf == 0) return;
-        wave_sync();
-        unsigned base = 0;
-        if (lane == 0) base = atomicAdd(n_rec, nbuf);
-        base = __builtin_amdgcn_readfirstlane(base);
+    // the buffered records go out at `base`; a record's fields come from its
+    // keypoint (sift.cpp:515-528)
+    auto write_out = [&](unsigned base) {
         for (unsigned i = lane; i < nbuf; i += 64) {
             const unsigned rec = base + i;
             if (rec >= cap_rec) continue;
@@ -1219,6 +1233,12 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             r.pori = eori[i];
             rec_side[rec] = RecSide{q.off0, q.img, 0};
         }
+    };
+    auto flush = [&]() {  // a full buffer: one counter atomic
+        wave_sync();
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(n_rec, nbuf);
+        write_out(__builtin_amdgcn_readfirstlane(base));
         wave_sync();
         nbuf = 0;
     };
@@ -1344,7 +1364,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             const unsigned long long m = __ballot(peak);
             if (!m) return;
             const unsigned c = (unsigned)__popcll(m);  // <= 64 = kOriEmit
-            if (nbuf + c > kOriEmit) flush();
+            if (nbuf + c > kOriEmit) flush();  // rare: 64 records
             if (peak) {
                 const unsigned i = nbuf + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
                 eori[i] = ori;
@@ -1439,7 +1459,20 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             k = k0 + n_waves + __builtin_amdgcn_readfirstlane(claim);
         }
     }
-    flush();
+    // the workgroup's remaining records: one counter atomic
+    __shared__ unsigned wg_n[4], wg_base[4];
+    if (lane == 0) wg_n[wv] = nbuf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = wg_n[0] + wg_n[1] + wg_n[2] + wg_n[3];
+        const unsigned base = t ? atomicAdd(n_rec, t) : 0u;
+        wg_base[0] = base;
+        wg_base[1] = base + wg_n[0];
+        wg_base[2] = wg_base[1] + wg_n[1];
+        wg_base[3] = wg_base[2] + wg_n[2];
+    }
+    __syncthreads();
+    write_out(wg_base[wv]);
 }
 
 // ---------------------------------------------------------------------------
