@@ -73,7 +73,9 @@ constexpr int kPairs = 2;
 constexpr int kCtrZeros = 4 * kLanes;
 constexpr int kCtrSnap = kCtrZeros + 4;
 constexpr int kCtrWork = kCtrSnap + 4 * (kMaxOctaves + 1);
-constexpr int kCtrWords = kCtrWork + 4 * (kMaxOctaves + 2);
+// then the record gather's checksum scratch: 64-bit accumulator + done count
+constexpr int kCtrGather = kCtrWork + 4 * (kMaxOctaves + 2);
+constexpr int kCtrWords = kCtrGather + 4;
 // largest per-lane capacities (the kernels index with 32-bit unsigned)
 constexpr size_t kMaxCand = (size_t)1 << 28;
 constexpr int kPipeHint = 16;  // submits a pipelining hint lasts
@@ -111,6 +113,7 @@ struct Mapped {
     int ensure(size_t n) {
         if (h && cap >= n) return SIFT_OK;
         release();
+        n = n < 1024 ? 1024 : n + n / 4;
         if (hipHostMalloc(&h, n * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess) {
             h = nullptr;
@@ -225,8 +228,9 @@ struct Slot {
     Pinned<sift_kp> h_ori;
     Pinned<RecSide> h_side;
     Pinned<float> h_df32;
-    Pinned<GatherItem> h_gather;  // fetch_device: (record index, size) per final record
-    DevBuf<GatherItem> d_gather;
+    // fetch_device: (record index, size) per final record, read by the gather
+    // kernel straight from mapped host memory (no copy launch)
+    Mapped<GatherItem> h_gather;
     // an asynchronous device fetch still reading this slot's records:
     // completed before the slot is reused (sift_hip_fetch_device_async)
     hipEvent_t gather_ev = nullptr;
@@ -1174,10 +1178,9 @@ void gather(Slot& s, sift_kp* out, float* df) {
 int gather_device(Slot& s, sift_kp* d_out, hipStream_t consumer, unsigned long long* checksum) {
     const size_t n = s.n_final;
     int st;
-    if (checksum) SIFT_HIP_TRY(hipMemsetAsync(checksum, 0, sizeof *checksum, s.sC));
+    if (n == 0 && checksum) SIFT_HIP_TRY(hipMemsetAsync(checksum, 0, sizeof *checksum, s.sC));
     if (n > 0) {
-        if ((st = s.h_gather.ensure(n)) != SIFT_OK || (st = s.d_gather.ensure(n)) != SIFT_OK)
-            return st;
+        if ((st = s.h_gather.ensure(n)) != SIFT_OK) return st;
         for (size_t i = 0; i < n; ++i) {
             const unsigned pos = s.keep[i];  // host position of the record
             int L;
@@ -1189,12 +1192,13 @@ int gather_device(Slot& s, sift_kp* d_out, hipStream_t consumer, unsigned long l
                 L = pos < s.n_lane[0] ? 0 : 1;
                 j = pos - (L ? s.n_lane[0] : 0);
             }
-            s.h_gather.p[i] = GatherItem{s.rec_src[pos].size, (unsigned)(L * s.cap_ori + j), 0};
+            s.h_gather.h[i] = GatherItem{s.rec_src[pos].size, (unsigned)(L * s.cap_ori + j), 0};
         }
-        SIFT_HIP_TRY(hipMemcpyAsync(s.d_gather.p, s.h_gather.p, n * sizeof(GatherItem),
-                                    hipMemcpyHostToDevice, s.sC));
-        SIFT_HIP_TRY(launch_gather_records(s.ori.p, s.d_gather.p, (unsigned)n, d_out, checksum,
-                                           s.sC));
+        // the checksum scratch words were zeroed with the job's counters
+        SIFT_HIP_TRY(launch_gather_records(
+            s.ori.p, s.h_gather.d, (unsigned)n, d_out, checksum,
+            reinterpret_cast<unsigned long long*>(s.d_ctr + kCtrGather), s.d_ctr + kCtrGather + 2,
+            s.sC));
     }
     if (!s.gather_ev)
         SIFT_HIP_TRY(hipEventCreateWithFlags(&s.gather_ev, hipEventDisableTiming));
@@ -1313,7 +1317,6 @@ int sift_hip_destroy(sift_ctx* ctx) {
         s.h_side.release();
         s.h_df32.release();
         s.h_gather.release();
-        s.d_gather.release();
         if (s.gather_ev) (void)hipEventDestroy(s.gather_ev);
         for (hipEvent_t e : s.chain_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : s.sync_ev) (void)hipEventDestroy(e);

@@ -80,7 +80,8 @@ hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* 
 
 // out[i] = recs[items[i].src] with size = items[i].size (final records on the device)
 hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, unsigned n,
-                                 sift_kp* out, unsigned long long* checksum, hipStream_t s);
+                                 sift_kp* out, unsigned long long* checksum,
+                                 unsigned long long* acc, unsigned* done, hipStream_t s);
 hipError_t launch_verify_slots(const void* slots, int n_slots, size_t slot_bytes, int hdr_rows,
                                int count_word, int sum_word, int n_sums, size_t cap_rows,
                                unsigned long long* bad, unsigned long long* acc, hipStream_t s);

@@ -1662,44 +1662,56 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 
 // Final records of a job gathered into the caller's HBM buffer
 // (sift_hip_fetch_device): out[i] = recs[items[i].src] with the host's
-// glibc-exact size (sift.cpp:427-429) at byte 24; with `checksum`, the
-// wrapping 64-bit sum of every word written is added to *checksum, so a
-// receiver of the records can verify them. Grid-stride over
-// the 21 words of every record (consecutive threads write consecutive words),
-// one checksum atomic per workgroup and at most kGatherWgs workgroups: a
-// wave per record with one atomic per workgroup of 4 records put ~1,500
-// same-address atomics (~10 ns each at one L2 channel) on a 1080p job.
+// glibc-exact size (sift.cpp:427-429) at byte 24; `items` is mapped host
+// memory (read over PCIe once per record, no copy launch). With `checksum`,
+// the wrapping 64-bit sum of every word written goes to *checksum so a
+// receiver can verify the records: one atomic per workgroup into `acc`
+// (zeroed with the job's counters), the last workgroup (`done`) writes the
+// total, so *checksum needs no memset launch. Grid-stride over the 21 words
+// of every record (consecutive threads write consecutive words), at most
+// kGatherWgs workgroups: a wave per record with one atomic per workgroup of
+// 4 records put ~1,500 same-address atomics (~10 ns each at one L2 channel)
+// on a 1080p job.
 constexpr unsigned kGatherWgs = 128;
 
 __global__ __launch_bounds__(256) void k_gather_records(const sift_kp* __restrict__ recs,
                                                         const GatherItem* __restrict__ items,
                                                         unsigned n, sift_kp* __restrict__ out,
-                                                        unsigned long long* __restrict__ checksum) {
+                                                        unsigned long long* __restrict__ checksum,
+                                                        unsigned long long* __restrict__ acc,
+                                                        unsigned* __restrict__ done) {
     __shared__ unsigned long long part[4];
     constexpr unsigned kWords = sizeof(sift_kp) / 8;  // 21
     const unsigned words = n * kWords;
-    unsigned long long acc = 0;
+    unsigned long long sum = 0;
     for (unsigned w = blockIdx.x * 256 + threadIdx.x; w < words; w += gridDim.x * 256) {
         const unsigned i = w / kWords, j = w - i * kWords;
         const GatherItem it = items[i];
         const double v = (j == 3) ? it.size : reinterpret_cast<const double*>(recs + it.src)[j];
         reinterpret_cast<double*>(out + i)[j] = v;
-        acc += (unsigned long long)__double_as_longlong(v);
+        sum += (unsigned long long)__double_as_longlong(v);
     }
     if (!checksum) return;
-    acc = wave_sum_u64(acc);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    sum = wave_sum_u64(sum);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(checksum, part[0] + part[1] + part[2] + part[3]);
+    if (threadIdx.x == 0) {
+        atomicAdd(acc, part[0] + part[1] + part[2] + part[3]);
+        // the add has returned (performed at the device coherence point)
+        // before the done increment is issued
+        __builtin_amdgcn_s_waitcnt(0);
+        if (atomicAdd(done, 1u) == gridDim.x - 1) *checksum = atomicAdd(acc, 0ull);
+    }
 }
 
 hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, unsigned n,
-                                 sift_kp* out, unsigned long long* checksum, hipStream_t s) {
+                                 sift_kp* out, unsigned long long* checksum,
+                                 unsigned long long* acc, unsigned* done, hipStream_t s) {
     if (n == 0) return hipSuccess;
     static_assert(sizeof(sift_kp) == 168, "21 words per record");
     const unsigned wgs = std::min<unsigned>(kGatherWgs, (n * 21u + 1023u) / 1024u);
     hipLaunchKernelGGL(k_gather_records, dim3(wgs), dim3(256), 0, s, recs, items, n, out,
-                       checksum);
+                       checksum, acc, done);
     return hipGetLastError();
 }
 
