@@ -282,7 +282,7 @@ struct sift_ctx {
     // job)
     unsigned* d_done = nullptr;
     unsigned prio_seq = 0;  // jobs whose k_job_done was enqueued (JobPrio.ticket)
-    DevBuf<unsigned long long> verify_acc;  // sift_hip_verify_slots: per-slot sums
+    DevBuf<unsigned long long> verify_acc;  // sift_hip_verify_slots: per-slot sum + count
     hipEvent_t verify_ev = nullptr;         // the last verify_slots call's end
     bool verify_used = false;
     // Streams of a job (submit_impl): a caller seen pipelining (pipe_hint:
@@ -1424,11 +1424,16 @@ int sift_hip_verify_slots(sift_ctx* ctx, const void* d_slots, int n_slots, size_
     // stream), and the scratch is regrown only after the last call finished
     if (!ctx->verify_ev)
         SIFT_HIP_TRY(hipEventCreateWithFlags(&ctx->verify_ev, hipEventDisableTiming));
-    const size_t need = (size_t)std::max(n_slots, 1);
+    // scratch: (accumulator, done count) per slot, left zeroed by every call
+    const size_t need = 2 * (size_t)std::max(n_slots, 1);
     if (ctx->verify_acc.cap < need && ctx->verify_used)
         SIFT_HIP_TRY(hipEventSynchronize(ctx->verify_ev));
+    const bool fresh = !ctx->verify_acc.p || ctx->verify_acc.cap < need;
     if (ctx->verify_acc.ensure(need) != SIFT_OK) return SIFT_ERR_NOMEM;
     if (ctx->verify_used) SIFT_HIP_TRY(hipStreamWaitEvent(st, ctx->verify_ev, 0));
+    if (fresh)
+        SIFT_HIP_TRY(hipMemsetAsync(ctx->verify_acc.p, 0,
+                                    ctx->verify_acc.cap * sizeof(unsigned long long), st));
     SIFT_HIP_TRY(launch_verify_slots(d_slots, n_slots, slot_bytes, hdr_rows, count_word, sum_word,
                                      n_sum_words, cap_rows,
                                      reinterpret_cast<unsigned long long*>(d_bad),

@@ -84,7 +84,8 @@ hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, u
                                  unsigned long long* acc, unsigned* done, hipStream_t s);
 hipError_t launch_verify_slots(const void* slots, int n_slots, size_t slot_bytes, int hdr_rows,
                                int count_word, int sum_word, int n_sums, size_t cap_rows,
-                               unsigned long long* bad, unsigned long long* acc, hipStream_t s);
+                               unsigned long long* bad, unsigned long long* scratch,
+                               hipStream_t s);
 
 // Matcher (sift_match.hip): records -> shifted descriptor rows + norms
 // (n_pad a multiple of 32, rows [n, n_pad) padding), then the 2-NN ratio test

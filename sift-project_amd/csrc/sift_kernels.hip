@@ -1720,66 +1720,66 @@ hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, u
 // rows, and at words [sum_word, sum_word + n_sums) the sender's checksums of
 // consecutive pieces of them (k_gather_records, one per step); the records'
 // wrapping word sum must equal the checksums' sum; a mismatch increments *bad.
-// Summing a slot of ~70 K records (1.5 M words) in one workgroup took 2.1 ms
-// per bucket on the exchange path (profiles/r03_m): k_verify_sum spreads each
-// slot over workgroups of kVerifyChunk words (four loads per thread in
-// flight, one 64-bit atomic per workgroup into the slot's accumulator; the
-// wrapping sum is order-free), k_verify_check compares one slot per
-// workgroup.
+// One launch: each workgroup sums kVerifyChunk words of one slot (four loads
+// per thread in flight) into the slot's accumulator with one 64-bit atomic;
+// the slot's last workgroup (done count) compares and resets the
+// accumulator and count for the next call (calls on a context are chained,
+// sift_hip_verify_slots). Summing a slot of ~70 K records in one workgroup
+// took 2.1 ms per bucket (profiles/r03_m); a memset + sum + check launch
+// triple per bucket: world-1 exchange step 1.036 -> 1.028x the plain step.
 constexpr int kVerifyChunk = 256 * 16;
 
-__global__ __launch_bounds__(256) void k_verify_sum(const unsigned long long* __restrict__ slots,
-                                                    size_t slot_words, int hdr_rows,
-                                                    int count_word, size_t cap_rows,
-                                                    unsigned long long* __restrict__ acc) {
+__global__ __launch_bounds__(256) void k_verify_slots(const unsigned long long* __restrict__ slots,
+                                                      size_t slot_words, int hdr_rows,
+                                                      int count_word, int sum_word, int n_sums,
+                                                      size_t cap_rows,
+                                                      unsigned long long* __restrict__ scratch,
+                                                      unsigned long long* __restrict__ bad) {
     __shared__ unsigned long long part[4];
-    const unsigned long long* sl = slots + (size_t)blockIdx.y * slot_words;
+    const unsigned slot = blockIdx.y;
+    const unsigned long long* sl = slots + (size_t)slot * slot_words;
     const unsigned long long n = sl[count_word];
     const size_t words = (size_t)(n < cap_rows ? n : cap_rows) * 21;
     const size_t k0 = (size_t)blockIdx.x * kVerifyChunk;
-    if (k0 >= words) return;  // whole workgroup
-    const unsigned long long* rec = sl + (size_t)hdr_rows * 21;
-    const size_t k1 = words - k0 < (size_t)kVerifyChunk ? words : k0 + kVerifyChunk;
     unsigned long long v = 0;
-    for (size_t k = k0 + threadIdx.x; k < k1; k += 4 * 256) {
-        unsigned long long a[4];
+    if (k0 < words) {
+        const unsigned long long* rec = sl + (size_t)hdr_rows * 21;
+        const size_t k1 = words - k0 < (size_t)kVerifyChunk ? words : k0 + kVerifyChunk;
+        for (size_t k = k0 + threadIdx.x; k < k1; k += 4 * 256) {
+            unsigned long long a[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] = k + q * 256 < k1 ? rec[k + q * 256] : 0ull;
+            for (int q = 0; q < 4; ++q) a[q] = k + q * 256 < k1 ? rec[k + q * 256] : 0ull;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v += a[q];
+            for (int q = 0; q < 4; ++q) v += a[q];
+        }
     }
     v = wave_sum_u64(v);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(&acc[blockIdx.y], part[0] + part[1] + part[2] + part[3]);
-}
-
-__global__ void k_verify_check(const unsigned long long* __restrict__ slots, size_t slot_words,
-                               int count_word, int sum_word, int n_sums, size_t cap_rows,
-                               const unsigned long long* __restrict__ acc,
-                               unsigned long long* __restrict__ bad) {
     if (threadIdx.x != 0) return;
-    const unsigned long long* sl = slots + (size_t)blockIdx.x * slot_words;
-    const unsigned long long n = sl[count_word];
+    unsigned long long* acc = scratch + 2 * slot;
+    unsigned long long* done = acc + 1;
+    atomicAdd(acc, part[0] + part[1] + part[2] + part[3]);
+    __builtin_amdgcn_s_waitcnt(0);  // the add has returned before the done count
+    if (atomicAdd(done, 1ull) != gridDim.x - 1) return;
+    const unsigned long long total = atomicAdd(acc, 0ull);
     unsigned long long want = 0;
     for (int k = 0; k < n_sums; ++k) want += sl[sum_word + k];
-    if (n > cap_rows || acc[blockIdx.x] != want) atomicAdd(bad, 1ull);
+    if (n > cap_rows || total != want) atomicAdd(bad, 1ull);
+    *acc = 0;  // ready for the next call (kernel boundary)
+    *done = 0;
 }
 
 hipError_t launch_verify_slots(const void* slots, int n_slots, size_t slot_bytes, int hdr_rows,
                                int count_word, int sum_word, int n_sums, size_t cap_rows,
-                               unsigned long long* bad, unsigned long long* acc, hipStream_t s) {
+                               unsigned long long* bad, unsigned long long* scratch,
+                               hipStream_t s) {
     if (n_slots <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(acc, 0, n_slots * sizeof(unsigned long long), s);
-    if (e != hipSuccess) return e;
     const auto* sl = static_cast<const unsigned long long*>(slots);
     const unsigned chunks =
         (unsigned)std::max<size_t>(1, (cap_rows * 21 + kVerifyChunk - 1) / kVerifyChunk);
-    hipLaunchKernelGGL(k_verify_sum, dim3(chunks, n_slots), dim3(256), 0, s, sl, slot_bytes / 8,
-                       hdr_rows, count_word, cap_rows, acc);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_verify_check, dim3(n_slots), dim3(64), 0, s, sl, slot_bytes / 8,
-                       count_word, sum_word, n_sums, cap_rows, acc, bad);
+    hipLaunchKernelGGL(k_verify_slots, dim3(chunks, n_slots), dim3(256), 0, s, sl, slot_bytes / 8,
+                       hdr_rows, count_word, sum_word, n_sums, cap_rows, scratch, bad);
     return hipGetLastError();
 }
 

@@ -237,6 +237,20 @@ def test_gpu_batch_record_exchange_world1(gpu_ctx):
             for i in ids:
                 assert res[10 * step + i].cpu().numpy().tobytes() == kps[i].tobytes(), (step, i)
         assert exb.step == 2 and exb.checked == 2 and exb.mismatches() == 0
+        # a flipped record byte is caught, and the check's scratch (left
+        # zeroed by every call) gives the restored slot a clean result again
+        g = exb.gathered[0]
+        rows = exb.cap + exb.hdr_rows
+        bad = torch.zeros(1, dtype=torch.int64, device=dev)
+        args = (g.data_ptr(), 1, rows * RECORD_BYTES, exb.hdr_rows, 1, exb.sum_word,
+                exb.bucket, exb.cap, bad.data_ptr())
+        for flip, want in ((False, 0), (True, 1), (True, 1), (False, 1)):
+            if flip:
+                g[exb.hdr_rows, 5] ^= 1
+            torch.cuda.synchronize()
+            gpu_ctx.verify_slots(*args)
+            torch.cuda.synchronize()
+            assert int(bad.item()) == want, (flip, want)
         # too small a destination keeps the job; then it can still be fetched
         t = gpu_ctx.submit(imgs[:1], INPUT_F64_HOST, 480, 360, 1)
         small = torch.empty((1, RECORD_BYTES), dtype=torch.uint8, device=dev)

@@ -2,7 +2,7 @@
 # exchange path at world size 1: plain vs --exchange, new gather vs previous
 # library, 400-step runs alternating; plus the GPU tests of the exchange
 set -o pipefail
-O=gpurun_out/r04_z
+O=gpurun_out/r04_aa
 mkdir -p $O
 P=sift-project_amd/alt/prev/libsift_hip.so
 timeout -k 10 600 python -u -m pytest tests/test_gpu_comm.py tests/test_gpu_batch.py -m gpu -x -q --timeout 300 \
