@@ -66,10 +66,9 @@ constexpr int kSlots = SIFT_MAX_INFLIGHT;
 constexpr int kPairs = 2;
 // device counter block of a slot: [4L..4L+3] live counters of lane L
 // (candidates, refined, records), [8..11] zeros, then per keypoint batch g a
-// 4-word snapshot taken by the last extrema workgroup (the batch's candidate
-// end and its raw / record begins, lane-local; word 3 = that launch's done
-// counter), then four words per chain: work and done counters of
-// orientation and descriptor
+// 4-word snapshot (the batch's candidate end, written by its refine launch,
+// and its raw / record begins, written by its extrema launch; lane-local),
+// then four words per chain: work counters of orientation and descriptor
 constexpr int kCtrZeros = 4 * kLanes;
 constexpr int kCtrSnap = kCtrZeros + 4;
 constexpr int kCtrWork = kCtrSnap + 4 * (kMaxOctaves + 1);
@@ -301,6 +300,8 @@ struct sift_ctx {
     // bursts). Launch graphs per slot cut the host's enqueue from 0.12 to
     // 0.03 ms per job but ran the step 2 % slower (profiles/r03_j): removed.
     int pipe_hint = 0;
+    long ext_waves = 512;   // SIFT_EXT_WAVES: extrema tasks per octave (extrema_grid)
+    int ext_seg_max = 32;   // SIFT_EXT_SEGMAX: centre rows per extrema task, at most
     // Pyramid token (SIFT_PYR_CHAIN): a job's pyramid waits for the previous
     // job's octave 0 (an event). In the steady state of a pipeline it is long
     // built; a burst of jobs submitted together (a pipeline filling) would
@@ -308,14 +309,12 @@ struct sift_ctx {
     // their latency-bound keypoint chains side by side, instead of the
     // staggered mix of the steady state, and the first job of the burst
     // finishes late.
-    long ext_waves = 512;   // SIFT_EXT_WAVES: extrema tasks per octave (extrema_grid)
-    int ext_seg_max = 32;   // SIFT_EXT_SEGMAX: centre rows per extrema task, at most
-    int pyr_chain = 1;  // 0 off; A/B: 2, 3 record the token later (enqueue_job)
-    // SIFT_LEAD_ALONE: a job submitted when none is in flight takes all four
-    // pair streams (two keypoint lanes) even in a pipelining caller, so the
-    // first job of a burst finishes at its alone latency; the jobs behind it
-    // take the other streams of the pool
-    bool lead_alone = false;
+    // (round 4: the token after the previous job's octave-0 keypoints or
+    // after its whole pyramid measured +15 % / +35 %, profiles/r04_ab r04_k)
+    bool pyr_chain = true;
+    // (round 4: SIFT_LEAD_ALONE, the first job of a burst on all four pair
+    // streams, finished it at 1.23 instead of 1.8 ms but queued the next
+    // three behind it: +2.7 % on the driver's bench, removed)
     int pyr_last = -1;  // slot of the last job that recorded its token
     // SIFT_DESC_MODE: 0 = k_descriptor_split, f64 sample math (default, the
     // reference's arithmetic); A/B only: 1 = k_descriptor_wave (f32 sample
@@ -470,8 +469,9 @@ void abandon(sift_ctx* ctx, Slot& s) {
 
 // One keypoint chain: extrema over octaves [o_begin, o_end) -> refine ->
 // orientation -> descriptor, on lane `lane`'s arrays and live counters, on
-// stream sx. `begin` (the snapshot written by the extrema launch's last
-// workgroup) holds this chain's candidate end and its raw / record begins;
+// stream sx. `begin` (the snapshot: raw / record begins written by the
+// extrema launch, candidate end by the refine launch) holds this chain's
+// candidate end and its raw / record begins;
 // candidates start at cand_begin (the lane's previous chain's snapshot);
 // nullptr: the live counters (overflow re-run).
 struct ChainSpec {
@@ -538,8 +538,10 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
         prof_events(ctx, s, &q0, &q1, 0.0, SIFT_PROF_ORIENT) != SIFT_OK ||
         prof_events(ctx, s, &d0, &d1, 0.0, SIFT_PROF_DESC) != SIFT_OK)
         return SIFT_ERR_HIP;
-    SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, begin ? begin : live + 0, cap_cand,
-                               raw, live + 1, cap_raw, sx, r0, r1));
+    // candidates [cand_begin, live[0]); the refine launch records that end in
+    // the chain's snapshot (begin[0]) for the lane's next chain
+    SIFT_HIP_TRY(launch_refine(d_pt, dp, cand, cand_begin, live + 0, cap_cand, raw, live + 1,
+                               cap_raw, begin, sx, r0, r1));
     SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
                                cap_ori, work, ori_wgs, alone, sx, q0, q1));
     SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
@@ -805,19 +807,11 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 SIFT_HIP_TRY(hipEventRecord(base_ready, so));
             }
         }
-        if (o == 0 && ctx->pyr_chain == 1) {
+        if (o == 0 && ctx->pyr_chain) {
             SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, so));
             ctx->pyr_last = (int)(&s - ctx->slots);
         }
         if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
-        if (o == 0 && ctx->pyr_chain == 2) {  // A/B: token after octave 0's keypoints
-            SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, lane_stream[0]));
-            ctx->pyr_last = (int)(&s - ctx->slots);
-        }
-    }
-    if (ctx->pyr_chain == 3) {  // A/B: token after the pyramid's strip-walk octaves
-        SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, pyr[(o_small - 1) & 1]));
-        ctx->pyr_last = (int)(&s - ctx->slots);
     }
     if (o_small < g.octaves) {
         hipStream_t so = pyr[o_small & 1];
@@ -1108,7 +1102,7 @@ int submit_impl(sift_ctx* ctx, const void* const* images, int n_images, int kind
         const bool hinted = ctx->pipe_hint > 0;
         if (others > 0) ctx->pipe_hint = kPipeHint;
         else if (ctx->pipe_hint > 0) --ctx->pipe_hint;
-        if (others > 0 || (hinted && !ctx->lead_alone)) {
+        if (others > 0 || hinted) {
             int k = 0;
             while (k + 1 < kSlots && (used >> k & 1u)) ++k;
             s.sA = s.sB = s.sC = s.sD = q[k];
@@ -1252,8 +1246,7 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_EXT_WAVES")) ctx->ext_waves = std::max(64L, std::atol(e));
     if (const char* e = std::getenv("SIFT_EXT_SEGMAX")) ctx->ext_seg_max = std::max(4, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e);
-    if (const char* e = std::getenv("SIFT_LEAD_ALONE")) ctx->lead_alone = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e) != 0;
     bool ok = prepare_kernel_attributes() == hipSuccess;
     ok = ok && hipMalloc(&ctx->d_done, sizeof(unsigned)) == hipSuccess &&
          hipMemset(ctx->d_done, 0, sizeof(unsigned)) == hipSuccess;

@@ -60,8 +60,8 @@ hipError_t launch_snapshot(const unsigned* ctr, unsigned* snap, hipStream_t s, i
                            int w1 = 4);
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
-                         RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s,
-                         hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                         RawKp* out, unsigned* n_out, unsigned cap_out, unsigned* snap0,
+                         hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // orientation of raw keypoints [*raw_begin, *n_raw) -> records appended at
 // n_rec; descriptors of records [*rec_begin, *n_rec). `work`: two zeroed
 // device words per launch (work counter, done counter); ex.cnt receives the

@@ -739,27 +739,16 @@ __global__ __launch_bounds__(256) void k_blur_cols_any(const double* __restrict_
 // or v == min(cube): v is itself in the cube, so the centre comparison is
 // vacuous (sift.cpp:241-246). DoG values are G_{l+1} - G_l computed on the fly.
 // ---------------------------------------------------------------------------
-// The last workgroup of an extrema launch to finish takes the lane's counter
-// snapshot for the keypoint chain (snap != nullptr: candidate end, raw /
-// record begins; snap[3] is the done counter).
-// No memory fence here, deliberately: every candidate atomic of a workgroup
-// has returned (it is performed at the device coherence point) before the
-// workgroup's done increment, so the last workgroup's atomic reads see the
-// final counts; the candidate records and the snapshot reach the next kernel
-// through the kernel boundary. (__threadfence() on gfx950 is an L2 writeback
-// + invalidate of the XCD: one per workgroup tripled the extrema time and
-// evicted the concurrent blurs' lines.)
-__device__ __forceinline__ void snapshot_if_last(unsigned* snap, const unsigned* live) {
-    __syncthreads();
-    if (snap && threadIdx.x == 0) {
-        const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
-        if (atomicAdd(&snap[3], 1u) == nblk - 1) {
-            snap[0] = atomicAdd(const_cast<unsigned*>(&live[0]), 0u);
-            snap[1] = atomicAdd(const_cast<unsigned*>(&live[1]), 0u);
-            snap[2] = atomicAdd(const_cast<unsigned*>(&live[2]), 0u);
-        }
-    }
-}
+// Chain snapshots (snap != nullptr): the extrema launch's first thread
+// records the lane's raw / record begins at its start (the previous chain on
+// the lane's stream has completed), k_refine's first thread records the
+// candidate end (the extrema launch has completed). Round 3 took all three
+// in the extrema launch's last workgroup, found by a done counter: one
+// same-address atomic per workgroup (~1,000 per 1080p octave-0 launch).
+// No memory fences in these kernels: __threadfence() on gfx950 is an L2
+// writeback + invalidate of the XCD (one per workgroup tripled the extrema
+// time and evicted the concurrent blurs' lines); the kernel boundary orders
+// the writes for the next kernel.
 
 // ---------------------------------------------------------------------------
 // k_extrema_stream<NL>: the same test (sift.cpp:227-291, window_size 3) as a
@@ -777,7 +766,7 @@ __device__ __forceinline__ void snapshot_if_last(unsigned* snap, const unsigned*
 // 48 B read per pixel and (62 + 2) / 62 x (kExtSeg + 2) / kExtSeg reuse.
 // Candidates: ballot per (row, layer) into a per-wave LDS buffer, one
 // counter atomic per wave. The last workgroup takes the lane snapshot
-// (snapshot_if_last). (A tiled variant staging 66x18 DoG halo tiles in LDS
+// (see Chain snapshots above). (A tiled variant staging 66x18 DoG halo tiles in LDS
 // was replaced by this scan in round 2 and removed in round 4.)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double dpp_from_left(double v) {  // lane i <- lane i-1
@@ -818,6 +807,12 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
     const int wv = threadIdx.x >> 6;
     const int task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
     const int b = blockIdx.y;
+    // the chain's raw / record begins: the lane's counters as the previous
+    // chain on this stream left them (its candidate end is taken by k_refine)
+    if (snap && blockIdx.x == 0 && b == 0 && threadIdx.x == 0) {
+        snap[1] = counter[1];
+        snap[2] = counter[2];
+    }
     sift_extremum* cb = cbuf[wv];
     unsigned nbuf = 0;  // wave-uniform
     if (task < eg.first_tile[eg.n]) {
@@ -945,7 +940,6 @@ __global__ __launch_bounds__(256) void k_extrema_stream(const PyrTable* __restri
     const unsigned base = wg_base[wv];
     for (unsigned i = lane; i < nbuf; i += 64)
         if (base + i < cap) out[base + i] = cb[i];
-    snapshot_if_last(snap, counter);
 }
 
 // Generic border b (window_size 4..7): one thread per (x, y), direct cube.
@@ -1087,8 +1081,11 @@ __global__ __launch_bounds__(NT) void k_refine(const PyrTable* __restrict__ pt, 
                                                const unsigned* __restrict__ n_cand,
                                                unsigned cap_cand, RawKp* __restrict__ out,
                                                unsigned* __restrict__ n_out,
-                                               unsigned cap_out) {
+                                               unsigned cap_out, unsigned* __restrict__ snap0) {
     set_job_prio(pt->jp, 0);
+    // the chain's candidate end (the extrema launch has completed) for the
+    // next chain on this lane
+    if (snap0 && blockIdx.x == 0 && threadIdx.x == 0) *snap0 = *n_cand;
     __shared__ RefineLds T;
     const unsigned n = min(*n_cand, cap_cand);
     const unsigned i0 = min(*cand_begin, n);
@@ -1843,8 +1840,8 @@ hipError_t launch_extrema_any(const PyrTable* d_pt, int o, int W, int H, int n_i
 
 hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_extremum* cand,
                          const unsigned* cand_begin, const unsigned* n_cand, unsigned cap_cand,
-                         RawKp* out, unsigned* n_out, unsigned cap_out, hipStream_t s,
-                         hipEvent_t e0, hipEvent_t e1) {
+                         RawKp* out, unsigned* n_out, unsigned cap_out, unsigned* snap0,
+                         hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     // one wavefront per workgroup, a candidate per lane: a batch's few
     // thousand candidates spread over ~100 CUs (256-thread workgroups, 16 or
     // 32 candidates per wave measured slower)
@@ -1852,7 +1849,7 @@ hipError_t launch_refine(const PyrTable* d_pt, const DevParams& P, const sift_ex
     unsigned blocks = (cap_cand + kPerWg - 1) / kPerWg;
     blocks = std::max(1u, std::min(blocks, 262144u / kPerWg));
     return launch_timed(k_refine<64, 64>, dim3(blocks), dim3(64), 0, s, e0, e1, d_pt, P, cand,
-                        cand_begin, n_cand, cap_cand, out, n_out, cap_out);
+                        cand_begin, n_cand, cap_cand, out, n_out, cap_out, snap0);
 }
 
 hipError_t launch_orient(const PyrTable* d_pt, const DevParams& P, const RawKp* raw,

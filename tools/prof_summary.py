@@ -16,9 +16,12 @@ def main(path, n_images=None):
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
         tot[r["Kernel_Name"]] += d
         cnt[r["Kernel_Name"]] += 1
-    # one counter memset (fillBuffer) opens every detect
+    # one counter memset (fillBuffer) opens every detect; one k_job_done
+    # closes every pipelined / serialised job (the image count when present)
     starts = [i for i, r in enumerate(rows) if "fillBuffer" in r["Kernel_Name"]]
-    n_img = n_images or max(1, len(starts))
+    n_done = sum(1 for r in rows if "k_job_done" in r["Kernel_Name"])
+    n_img = n_images or max(1, n_done or len(starts))
+    print(f"{n_img} images")
     print(f"{'kernel':40s} {'calls':>6s} {'total us':>10s} {'avg us':>9s} {'us/image':>9s}")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"{k[:40]:40s} {cnt[k]:6d} {v:10.1f} {v / cnt[k]:9.2f} {v / n_img:9.1f}")
