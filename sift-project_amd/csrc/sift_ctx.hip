@@ -253,14 +253,16 @@ struct sift_ctx {
     // A/B on 1080p, single-image jobs four in flight: 192 per image 0.521
     // ms, 256 0.527, 512 0.548; 8-image jobs 0.503 ms per image at 512 in
     // all vs 0.537 at 1024). Round 4 with the f64 split descriptor (one
-    // record per workgroup): orientation 128 / descriptor 256 per image
-    // -1.1 % against 192 / 384 (512 descriptor workgroups +1.3 %, 384
-    // orientation workgroups +3.8 %). A job alone on the chip gets the same
-    // grid (1024 workgroups starved the concurrent small-octave blurs on its
-    // critical path) except for its last chain (enqueue_chain). SIFT_KP_WGS /
+    // record per workgroup) and dynamic claims on every item: 128 / 256
+    // measured -1.1 % against 192 / 384; once each workgroup's first item
+    // was static and the extrema / orientation flushes per workgroup, 192 /
+    // 384 came back ahead: -2.3 % over 6 interleaved runs of the driver's
+    // command (profiles/r04_ab r04_ee; 512 descriptor workgroups +0.7 %,
+    // 96 orientation +1.5 %). Jobs alone: x1.5, or the whole chip for a
+    // launch with nothing beside it (enqueue_chain). SIFT_KP_WGS /
     // SIFT_DESC_WGS (tuning).
-    unsigned kp_wgs = 128;
-    unsigned desc_wgs = 256;  // k_descriptor_split: ONE record per workgroup
+    unsigned kp_wgs = 192;
+    unsigned desc_wgs = 384;  // k_descriptor_split: ONE record per workgroup
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
     // rest form one final batch after the LDS octaves. A single-image job
     // sharing the chip (one stream, lanes = 1) uses 2^22: a 1080p job has two
