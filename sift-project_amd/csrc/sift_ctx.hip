@@ -274,8 +274,15 @@ struct sift_ctx {
     int batch_px_log2 = 22;
     int batch_px_log2_alone = 18;
     // octaves of at most this many pixels (and within the LDS, lds_octave_fits)
-    // run LDS-resident in the one-workgroup k_octaves_lds (SIFT_LDS_PX, tests)
+    // run LDS-resident in the one-workgroup k_octaves_lds (SIFT_LDS_PX, tests:
+    // both). A single-image job sharing the chip takes every octave that
+    // fits (1080p: from octave 5, 120x67, on): five fewer launches in its
+    // chain, -1.2 % on the driver's bench (profiles/r04_ab r04_ff); jobs
+    // alone keep octave 5 on tile launches over the chip (kernel-alone
+    // octave 5: 23 us over five launches vs ~29 us of the one-CU kernel,
+    // which then takes 76 instead of 47 us; synchronous latency)
     size_t lds_max_px = kLdsOctaveMaxPx;
+    size_t lds_max_px_shared = kLdsOctavePx;
     bool serial = false;  // SIFT_SERIAL=1: every kernel on one stream (profiling)
     // Kernels raise their waves' issue priority by their job's age rank
     // (JobPrio; -1.3 % on the driver's bench command, round 3); d_done
@@ -713,8 +720,10 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // octaves from o_small on are small enough to run LDS-resident in one
     // launch (k_octaves_lds); the larger ones get one k_blur launch per level
     int o_small = g.octaves;
+    const size_t lds_px = (s.lanes == 1 && n_img == 1 && !ctx->serial) ? ctx->lds_max_px_shared
+                                                                        : ctx->lds_max_px;
     for (int o = 0; o < g.octaves; ++o)
-        if (lds_octave_fits(g.W[o], g.H[o]) && (size_t)(g.W[o] | 1) * g.H[o] <= ctx->lds_max_px) {
+        if (lds_octave_fits(g.W[o], g.H[o]) && (size_t)(g.W[o] | 1) * g.H[o] <= lds_px) {
             o_small = o;
             break;
         }
@@ -1245,7 +1254,10 @@ int sift_hip_create(int device, sift_ctx** out) {
     }
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
-    if (const char* e = std::getenv("SIFT_LDS_PX")) ctx->lds_max_px = (size_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_LDS_PX"))
+        ctx->lds_max_px = ctx->lds_max_px_shared = (size_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_LDS_PX_SHARED"))
+        ctx->lds_max_px_shared = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_EXT_WAVES")) ctx->ext_waves = std::max(64L, std::atol(e));
     if (const char* e = std::getenv("SIFT_EXT_SEGMAX")) ctx->ext_seg_max = std::max(4, std::atoi(e));
     if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e) != 0;
