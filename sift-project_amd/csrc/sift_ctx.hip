@@ -534,14 +534,14 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     // chain of a serialised context: those fill the chip (kKpWgsMax
     // orientation workgroups, kDescWgsAlone one-record descriptor
     // workgroups = every resident slot). The other chains of a job alone
-    // overlap its own smaller octaves' blurs: 1.5x the shared grid
+    // overlap its own smaller octaves' blurs and take the shared grid (1.5x
+    // of 192 / 384 delayed the small octaves behind them: synchronous latency
+    // 0.86 vs 0.82-0.84 ms, profiles/r04_final/summary_lat.txt)
     const bool alone = ctx->serial || (s.lanes > 1 && o_end == g.octaves);
-    const unsigned scale2 = s.lanes > 1 ? 3u : 2u;  // x1.5 for a job alone, in halves
     const unsigned ori_wgs =
-        alone ? kKpWgsMax : std::min(kKpWgsMax, ctx->kp_wgs * scale2 / 2u * (unsigned)n_img);
+        alone ? kKpWgsMax : std::min(kKpWgsMax, ctx->kp_wgs * (unsigned)n_img);
     const unsigned desc_wgs =
-        alone ? kDescWgsAlone
-              : std::min(kKpWgsMax, ctx->desc_wgs * scale2 / 2u * (unsigned)n_img);
+        alone ? kDescWgsAlone : std::min(kKpWgsMax, ctx->desc_wgs * (unsigned)n_img);
     hipEvent_t r0, r1, q0, q1, d0, d1;  // profiling events of the keypoint stages
     if (prof_events(ctx, s, &r0, &r1, 0.0, SIFT_PROF_REFINE) != SIFT_OK ||
         prof_events(ctx, s, &q0, &q1, 0.0, SIFT_PROF_ORIENT) != SIFT_OK ||
