@@ -28,8 +28,11 @@ def main(paths, detects):
 
 
 if __name__ == "__main__":
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv = sys.argv[1:]
     n = 7
-    if "--detects" in sys.argv:
-        n = int(sys.argv[sys.argv.index("--detects") + 1])
+    if "--detects" in argv:
+        i = argv.index("--detects")
+        n = int(argv[i + 1])
+        del argv[i:i + 2]
+    args = [a for a in argv if not a.startswith("--")]
     main(args, n)
