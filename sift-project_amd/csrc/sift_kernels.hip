@@ -163,8 +163,8 @@ __global__ __launch_bounds__(256) void k_prepare(const double* __restrict__ in, 
 //    pass of yy; tools/blur_lab.hip IL variants);
 //  * the window slot of every row is a compile-time constant (the step loop
 //    is unrolled by the window depth), so the window never moves.
-// Every lane issues every load and store (rows clamped; out-of-image
-// outputs go to a per-wave trash line). Replicate borders: staged columns and
+// Every lane issues every load (rows clamped); out-of-image lanes skip
+// their store. Replicate borders: staged columns and
 // source rows are clamped, i.e. the reference's min(x+u, W-1) / max(x-u, 0)
 // (image.cpp:177-180, 200-203). DECIM also writes resize_inter_nearest
 // (image.cpp:41-55) of the output, the next octave's base (sift.cpp:195-196).
@@ -181,7 +181,6 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
     constexpr int SPAN = 64 * C;                   // strip width
     constexpr int NL = (SPAN + 2 * R + 63) / 64;   // staged loads per lane per row
     __shared__ __attribute__((aligned(16))) double sline[4][64 * NL + 2];
-    __shared__ __attribute__((aligned(16))) double trash[4][SPAN];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int bx, by, bz;
@@ -346,12 +345,16 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
                                          win[c][(s + R + 1 + NW - u) % NW]);
                         o[c] = div_sum_w(a, sw, inv);
                     }
-                    if (C == 2) {  // W is even for C == 2 (launcher)
-                        double* d = (xa < W) ? dst + (size_t)y * W + xa : &trash[wv][2 * lane];
-                        *reinterpret_cast<double2*>(d) = make_double2(o[0], o[C - 1]);
-                    } else {
-                        double* d = (xa < W) ? dst + (size_t)y * W + xa : &trash[wv][lane];
-                        *d = o[0];
+                    // guarded global store (round 4: an LDS trash line for
+                    // the out-of-image lanes made the store FLAT, which counts
+                    // in lgkmcnt, so every step's LDS wait also waited for the
+                    // store: octave 0 alone -1.3 %, latency -1.5 %, r04_ii)
+                    if (xa < W) {
+                        if (C == 2)  // W is even for C == 2 (launcher)
+                            *reinterpret_cast<double2*>(dst + (size_t)y * W + xa) =
+                                make_double2(o[0], o[C - 1]);
+                        else
+                            dst[(size_t)y * W + xa] = o[0];
                     }
                     if (DECIM && !(y & 1) && (y >> 1) < Hd) {
                         // the even column of the lane: xa for C == 2, x for C == 1
