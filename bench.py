@@ -38,6 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # stream each), two 8-image jobs (a stream pair each)
 JOB_DEPTH = max(1, min(8, int(os.environ.get("SIFT_JOB_DEPTH", "4"))))
 BATCH_DEPTH = max(1, min(8, int(os.environ.get("SIFT_BATCH_DEPTH", "2"))))
+# BASELINE configs 3 / 5: one large image per job, jobs in flight
+BIG_DEPTH = max(1, min(8, int(os.environ.get("SIFT_BIG_DEPTH", "2"))))
 sys.path.insert(0, os.path.join(ROOT, "sift-project_amd"))
 
 import numpy as np  # noqa: E402
@@ -217,14 +219,14 @@ def chip_roofline(bytes_img: float, launches_img: float, images: int, elapsed: f
 # reference-generated goldens tests/golden/synth_4096x4096_int2_oct5.npz and
 # synth_7680x4320_dense.npz, which pin the HIP path's output on them)
 BIG_CONFIGS = {
-    "config3": {"w": 4096, "h": 4096, "nblobs": 300000, "smax": 6.0, "images": 8,
+    "config3": {"w": 4096, "h": 4096, "nblobs": 300000, "smax": 6.0, "images": 16,
                 "params": {"intervals": 2, "max_octaves": 5},
                 "workload": "BASELINE config 3: single 4096x4096 synthetic image (seed 42, 300k "
                             "blobs), 5 octaves x 5 scales (intervals=2, max_octaves=5)",
                 "reference_cpu": {"seconds": 109.7, "keypoints": 46242,
                                   "source": "BASELINE.md (survey container, copy-fixed reference, "
                                             "1 thread)"}},
-    "config5": {"w": 7680, "h": 4320, "nblobs": 1500000, "smax": 4.0, "images": 5,
+    "config5": {"w": 7680, "h": 4320, "nblobs": 1500000, "smax": 4.0, "images": 12,
                 "params": {},
                 "workload": "BASELINE config 5: 8K (7680x4320) dense synthetic image (seed 42, "
                             "1.5M blobs), reference default parameters",
@@ -235,9 +237,10 @@ BIG_CONFIGS = {
 
 
 def big_config_leg(name: str, dev) -> dict:
-    """One large image per job, JOB pairs in flight (two jobs: the next
-    image's pyramid overlaps the previous one's keypoint tail), input
-    resident in HBM: keypoints/s and ms per image; the pyramid's chip-level
+    """One large image per job, BIG_DEPTH jobs in flight (the next image's
+    pyramid overlaps the previous one's keypoint tail), input resident in
+    HBM, after a warm-up that ran a job in every slot the pipeline cycles
+    through: keypoints/s and ms per image, the library's host phases per job; the pyramid's chip-level
     HBM fraction over that time, its kernel-alone fraction and FP64-issue
     fraction (SIFT_SERIAL context, dispatch-timestamped events), and the
     keypoint kernels alone."""
@@ -250,9 +253,14 @@ def big_config_leg(name: str, dev) -> dict:
     ptr = [t.data_ptr()]
     c = Context(dev.index)
     sub = lambda k: c.submit(ptr, INPUT_F64_DEVICE, w, h, 1, p)  # noqa: E731
-    pipelined(c, sub, 2, 2)
+    depth = BIG_DEPTH
+    # warm-up: every slot a depth-d pipeline cycles through (d + 1) has run a
+    # job, so the timed jobs find their buffers allocated
+    pipelined(c, sub, depth + 2, depth)
     n = spec["images"]
-    kp, dt = pipelined(c, sub, n, 2)
+    phases = collections.Counter()
+    kp, dt = pipelined(c, sub, n, depth,
+                       on_fetch=lambda: phases.update(c.host_timing()))
     cnt = c.counts()
     c.close()
     dims = [(cnt["octave0_w"] >> o, cnt["octave0_h"] >> o) for o in range(cnt["octaves"])]
@@ -285,7 +293,14 @@ def big_config_leg(name: str, dev) -> dict:
             "fp64": {"ops_per_image": fp64, "peak_ops_per_s": FP64_PEAK_OPS,
                      "frac": fp64 * n / dt / FP64_PEAK_OPS,
                      "frac_alone": fp64 / (pyr["us_per_image"] * 1e-6) / FP64_PEAK_OPS}}
-    return {"workload": spec["workload"], "image": f"{w}x{h}x1", "images": n, "jobs_in_flight": 2,
+    host = {k: v / n for k, v in phases.items()}
+    return {"workload": spec["workload"], "image": f"{w}x{h}x1", "images": n,
+            "jobs_in_flight": depth,
+            "host_phases_ms": dict(host, note="per job, library host phases: enqueue "
+                                   "(launches), wait_device (chain runs sorted while waiting), "
+                                   "download (bulk path only), finalize (merge + unique), "
+                                   "output (records into the caller's array), blocked (host "
+                                   "waiting on device events)"),
             "value": kp / dt, "unit": "keypoints/s", "ms_per_image": dt / n * 1e3,
             "keypoints_per_image": kp // n, "octaves": cnt["octaves"],
             "levels_per_octave": cnt["levels_per_octave"], "dtype": "f64",
@@ -393,44 +408,6 @@ def alone_leg(dev_img, W, H, params, n_images: int = 200, batch_imgs=None) -> di
     return out
 
 
-def desc_modes_leg(ptrs, W, H, params, n_steps: int, depth: int, rounds: int = 4) -> dict:
-    """The timed region's pipelined step on fresh contexts whose descriptor
-    kernel runs in SIFT_DESC_MODE 0 (the default: k_descriptor_split, every
-    per-sample operation in f64 as src/sift.cpp:641-678) and 1 (round 3's
-    k_descriptor_wave, f32 sample math), in interleaved blocks (the boxes
-    drift by several % run to run; the ratio holds)."""
-    prev = os.environ.get("SIFT_DESC_MODE")
-    ctxs = {}
-    try:
-        for mode in (0, 1):
-            os.environ["SIFT_DESC_MODE"] = str(mode)
-            ctxs[mode] = Context(torch.cuda.current_device())
-    finally:
-        if prev is None:
-            os.environ.pop("SIFT_DESC_MODE", None)
-        else:
-            os.environ["SIFT_DESC_MODE"] = prev
-    kp = {m: 0 for m in ctxs}
-    dt = {m: 0.0 for m in ctxs}
-    block = max(1, n_steps // rounds)
-    for m, c in ctxs.items():
-        pipelined(c, lambda k, c=c: c.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params),
-                  4 * depth, depth)
-    for r in range(rounds):
-        for m in ((0, 1) if r % 2 == 0 else (1, 0)):
-            c = ctxs[m]
-            k, t = pipelined(c, lambda k, c=c: c.submit(ptrs, INPUT_F64_DEVICE, W, H, 1, params),
-                             block, depth)
-            kp[m] += k
-            dt[m] += t
-    for c in ctxs.values():
-        c.close()
-    return {f"desc_mode_{m}": {"value": kp[m] / dt[m], "unit": "keypoints/s",
-                               "ms_per_step": dt[m] / (block * rounds) * 1e3,
-                               "steps": block * rounds}
-            for m in (0, 1)}
-
-
 def host_busy_leg(ctx, ptrs, W, H, params, n_steps: int, depth: int) -> dict:
     """Where the host's time goes in the pipelined loop (after the timed
     region): wall time inside submit() (plan + enqueue, pure host) and inside
@@ -465,9 +442,10 @@ def host_busy_leg(ctx, ptrs, W, H, params, n_steps: int, depth: int) -> dict:
                     "caller's array)"}
 
 
-def pipelined(ctx, submit, n_steps: int, depth: int = 0):
+def pipelined(ctx, submit, n_steps: int, depth: int = 0, on_fetch=None):
     """Run n_steps jobs with `depth` (default JOB_DEPTH) in flight: job k+d-1
-    is submitted before job k is fetched; returns (keypoints, elapsed s)."""
+    is submitted before job k is fetched; returns (keypoints, elapsed s).
+    on_fetch() runs after every fetch (inside the time)."""
     depth = depth or JOB_DEPTH
     kp = 0
     t0 = time.perf_counter()
@@ -477,6 +455,8 @@ def pipelined(ctx, submit, n_steps: int, depth: int = 0):
             q.append(submit(k + len(q)))
         kps, _ = ctx.fetch(q.popleft())
         kp += sum(len(x) for x in kps)
+        if on_fetch is not None:
+            on_fetch()
     return kp, time.perf_counter() - t0
 
 
@@ -574,6 +554,29 @@ def stitch_leg(ctx, seconds: float) -> dict:
                     "stitch-graph edges"}
 
 
+def launch_workers(n_gpus: int, json_out) -> int:
+    """bench.py --gpus N (N > 1) run directly: one worker per GPU through
+    torch.distributed.run as child processes (127.0.0.1 rendezvous on a free
+    port), exactly the driver's multi-GPU command; rank 0's JSON line is
+    forwarded to stdout and the launcher's exit status returned. Nothing in
+    this process touches the GPU."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n_gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print("launching: " + " ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if lines:
+        print(lines[-1], file=json_out, flush=True)
+    return r.returncode
+
+
 def main() -> int:
     # stdout carries exactly one JSON line: keep a handle on it and send
     # fd 1 to stderr for everything else (RCCL prints its banner to stdout)
@@ -599,10 +602,6 @@ def main() -> int:
                          "cost amortised over a bucket of steps)")
     ap.add_argument("--sync", action="store_true",
                     help="one job at a time (no pipelining), for profiling / A-B")
-    ap.add_argument("--no-desc-f64", action="store_true",
-                    help="(kept for old command lines: the default descriptor is all-f64)")
-    ap.add_argument("--desc-ab", action="store_true",
-                    help="steady-state A/B of the descriptor variants (desc_modes_leg)")
     ap.add_argument("--no-big", action="store_true",
                     help="skip the BASELINE config 3 / config 5 legs (4096^2, 8K)")
     ap.add_argument("--no-extra", action="store_true",
@@ -623,12 +622,18 @@ def main() -> int:
                          "while its kernel-source hash matches the sources")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launched without torchrun: start one fresh worker process per GPU
+        # (before anything here touched the GPU) and pass the JSON line on
+        json_out.flush()
+        return launch_workers(args.gpus, json_out)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
-              file=sys.stderr)
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+              f"different GPU count than asked for", file=sys.stderr)
+        return 2
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     use_exchange = world > 1 or args.exchange
@@ -829,7 +834,7 @@ def main() -> int:
             "dtype": "f64",
             "dtype_note": ("every stage in f64 as the reference: pyramid, DoG, extrema, refine, "
                            "orientation and the descriptor's per-sample math (rotation, "
-                           "magnitude, atan2, exp, trilinear weights; desc_mode 0) with f64 "
+                           "magnitude, atan2, exp, trilinear weights) with f64 "
                            "histograms"),
             "data": "synthetic (deterministic integer-RNG generator: sinusoid + Gaussian blobs, "
                     "~w*h/52 blobs, sigma 1.5-7.5)",
@@ -840,7 +845,6 @@ def main() -> int:
                 "image": f"{W}x{H}x1",
                 "images_per_gpu_per_step": B,
                 "jobs_in_flight": depth,
-                "desc_mode": int(os.environ.get("SIFT_DESC_MODE", "0")),
                 "keypoints_per_image": kp_per_image,
                 "parallelism": f"image-sharded x{world}" + (
                     ", RCCL all-gather of the descriptor records straight from HBM "
@@ -874,8 +878,6 @@ def main() -> int:
             out["keypoint_kernels_alone_batch8"] = alone["batch"]["keypoint_kernels"]
         if world == 1 and not args.no_extra:
             out["host_busy"] = host_busy_leg(ctx, ptrs, W, H, params, max(args.steps, 400), depth)
-        if world == 1 and args.desc_ab:
-            out["desc_modes_leg"] = desc_modes_leg(ptrs, W, H, params, max(args.steps, 800), depth)
         if exchange_check is not None:
             out["exchange_check"] = exchange_check
         if world == 1 and not args.no_extra:

@@ -39,6 +39,8 @@ extern "C" {
 #define SIFT_ERR_PARAM -7        /* parameter outside the supported range      */
 #define SIFT_ERR_STATE -8        /* call order violated (e.g. no prior detect) */
 #define SIFT_ERR_NO_COMM -9      /* RCCL missing or a collective failed        */
+#define SIFT_ERR_PEER -10        /* another rank of a collective failed; this
+                                    rank joined every collective and returns */
 
 /*
  * Parameters of detect_keypoints_and_descriptors (reference sift.hh:65-71),
@@ -229,16 +231,23 @@ int sift_hip_comm_init_all(int n_devices, const int* devices, sift_comm** comms)
 int sift_hip_comm_destroy(sift_comm* comm);
 int sift_hip_comm_rank(const sift_comm* comm, int* rank, int* nranks);
 
-/* Collective over every rank of `comm` (each rank calls it once, with the
- * same max_local). This rank's n_local (<= max_local) images: image ids[j]
- * has counts[j] final records, image-major in d_recs (device memory, e.g.
- * from sift_hip_fetch_device). On return every rank's d_out (device, cap_out
+/* Collective over every rank of `comm` (each rank calls it once). max_local
+ * is a collective argument like an all-gather's count: every rank passes the
+ * same value (checked: a mismatch returns SIFT_ERR_ARG on every rank). This
+ * rank's n_local (<= max_local) images: image ids[j] has counts[j] final
+ * records, image-major in d_recs (device memory, e.g. from
+ * sift_hip_fetch_device). On return every rank's d_out (device, cap_out
  * records) holds all ranks' records rank-major (rank 0's images in its
  * order, then rank 1's, ...), *n_out their total, and the host arrays
  * out_ids / out_counts (nranks * max_local entries, rank-major, id -1 for an
  * empty entry) describe them. Blocking (the host waits for the counts and
  * the final copies); `stream` optional. *n_out > cap_out: SIFT_ERR_ARG after
- * the collectives completed, nothing written to d_out. */
+ * the collectives completed, nothing written to d_out.
+ * No local failure leaves a peer blocked: a rank with a bad argument, or one
+ * that cannot allocate or stage its payload, still enters every collective
+ * of the call; the ranks agree on the failure before the payload moves, the
+ * failing rank returns its own error and the others SIFT_ERR_PEER
+ * (csrc/sift_exchange.h). */
 int sift_hip_allgather_records(sift_comm* comm, const sift_kp* d_recs, const int64_t* ids,
                                const size_t* counts, int n_local, int max_local, sift_kp* d_out,
                                size_t cap_out, int64_t* out_ids, size_t* out_counts,

@@ -182,4 +182,8 @@ bool host_pack_u8(const double* src, size_t n, uint8_t* dst) {
     return true;
 }
 
+void host_parallel(unsigned n_tasks, const std::function<void(unsigned)>& fn) {
+    pool().run(n_tasks, fn);
+}
+
 }  // namespace sift_amd

@@ -325,10 +325,12 @@ struct sift_ctx {
     // streams, finished it at 1.23 instead of 1.8 ms but queued the next
     // three behind it: +2.7 % on the driver's bench, removed)
     int pyr_last = -1;  // slot of the last job that recorded its token
-    // SIFT_DESC_MODE: 0 = k_descriptor_split, f64 sample math (default, the
-    // reference's arithmetic); A/B only: 1 = k_descriptor_wave (f32 sample
-    // math, a wavefront per record), 2 = k_descriptor_split with f32 math
-    int desc_mode = 0;
+    // records per lane per octave-0 pixel, the largest any finalised job of
+    // this context had: a slot's first job sizes its mapped export buffers
+    // from it (otherwise a cold slot's first job overflows the default size
+    // and falls back to the bulk download + a full host sort: 12-17 ms on an
+    // 8K image, the first two jobs of every config-5 leg in round 4)
+    double exp_px_hint = 0.0;
     Slot slots[kSlots];
     // two stream pairs, one per hardware queue each (HIP's default is four
     // queues per process): pair k = pyramid (high priority) + keypoint chains
@@ -472,6 +474,7 @@ void abandon(sift_ctx* ctx, Slot& s) {
     for (int k = 2 * kPairs; k < kSlots; ++k)
         if (ctx->pool[k]) (void)hipStreamSynchronize(ctx->pool[k]);
     s.pending.clear();
+    s.gather_pending = false;  // every stream drained: no gather still reads the slot
     s.state = kFree;
     s.ticket = -1;
 }
@@ -554,7 +557,7 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     SIFT_HIP_TRY(launch_orient(d_pt, dp, raw, b + 1, live + 1, cap_raw, recs, side, live + 2,
                                cap_ori, work, ori_wgs, alone, sx, q0, q1));
     SIFT_HIP_TRY(launch_descriptor(d_pt, dp, recs, side, b + 2, live + 2, cap_ori, df32,
-                                   work + 2, c.ex, desc_wgs, ctx->desc_mode, sx, d0, d1));
+                                   work + 2, c.ex, desc_wgs, sx, d0, d1));
     return SIFT_OK;
 }
 
@@ -746,7 +749,10 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // records of every chain also go to the mapped export buffers, sized from
     // the largest record count seen so far (a larger one falls back to one
     // bulk download at the end, and grows them for the next call)
-    const size_t exp_want = std::max<size_t>(s.exp_rec.cap, (size_t)8192 * n_img * kLanes);
+    const size_t exp_hint =
+        (size_t)(ctx->exp_px_hint * 1.5 * (double)W0 * (double)H0 * n_img) * kLanes;
+    const size_t exp_want =
+        std::max<size_t>({s.exp_rec.cap, (size_t)8192 * n_img * kLanes, exp_hint});
     if ((st = s.exp_rec.ensure(exp_want)) != SIFT_OK ||
         (st = s.exp_side.ensure(s.exp_rec.cap)) != SIFT_OK ||
         (st = s.exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
@@ -951,6 +957,9 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
         n_ori += s.n_lane[L];
     }
     if (s.exported && s.n_keys != n_ori) s.exported = false;
+    ctx->exp_px_hint = std::max(ctx->exp_px_hint,
+                                (double)std::max(s.n_lane[0], s.n_lane[1]) /
+                                    ((double)g.W[0] * (double)g.H[0] * s.n_img));
     s.rec_src = s.exp_rec.h;
     // host position of lane L's record i: exported, L * exp_lane + i; after a
     // bulk download, the lanes are concatenated
@@ -1167,11 +1176,23 @@ void gather(Slot& s, sift_kp* out, float* df) {
     const auto t0 = clk::now();
     // record i's host row: exported -> lane-local index already offset by
     // host_base at export time (keep holds host positions); bulk -> concatenated
-    if (out)
-        for (size_t i = 0; i < s.n_final; ++i) out[i] = s.rec_src[s.keep[i]];
-    if (df && s.want_df)
-        for (size_t i = 0; i < s.n_final; ++i)
-            std::memcpy(df + i * 128, s.h_df32.p + (size_t)s.keep[i] * 128, 128 * sizeof(float));
+    // large outputs (config 5: 166 k records = 28 MB, much of it first
+    // touches of the caller's fresh pages) on the host pool's threads
+    constexpr size_t kPiece = 8192;
+    const size_t n = s.n_final;
+    const unsigned pieces = (unsigned)((n + kPiece - 1) / kPiece);
+    auto copy = [&](unsigned t) {
+        const size_t b = (size_t)t * kPiece, e = std::min(n, b + kPiece);
+        if (out)
+            for (size_t i = b; i < e; ++i) out[i] = s.rec_src[s.keep[i]];
+        if (df && s.want_df)
+            for (size_t i = b; i < e; ++i)
+                std::memcpy(df + i * 128, s.h_df32.p + (size_t)s.keep[i] * 128,
+                            128 * sizeof(float));
+    };
+    if (pieces > 2) host_parallel(pieces, copy);
+    else
+        for (unsigned t = 0; t < pieces; ++t) copy(t);
     s.t_host[4] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
 }
 
@@ -1253,7 +1274,6 @@ int sift_hip_create(int device, sift_ctx** out) {
         if (v >= 0 && v <= 40) ctx->batch_px_log2 = ctx->batch_px_log2_alone = v;
     }
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SIFT_DESC_MODE")) ctx->desc_mode = std::atoi(e);
     if (const char* e = std::getenv("SIFT_LDS_PX"))
         ctx->lds_max_px = ctx->lds_max_px_shared = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_LDS_PX_SHARED"))
@@ -1388,11 +1408,15 @@ int sift_hip_fetch_device(sift_ctx* ctx, int ticket, void* d_out, size_t cap) {
     if (cap < s->n_final) return SIFT_ERR_ARG;  // the job stays fetchable
     (void)hipSetDevice(ctx->device);
     st = gather_device(*s, static_cast<sift_kp*>(d_out), nullptr, nullptr);
-    if (st == SIFT_OK) SIFT_HIP_TRY(hipEventSynchronize(s->gather_ev));
+    if (st == SIFT_OK && hipEventSynchronize(s->gather_ev) != hipSuccess) st = SIFT_ERR_HIP;
+    if (st != SIFT_OK) {  // as fetch_device_async: drain and release the job
+        abandon(ctx, *s);
+        return st;
+    }
     s->gather_pending = false;
     s->state = kFree;
     s->ticket = -1;
-    return st;
+    return SIFT_OK;
 }
 
 int sift_hip_fetch_device_async(sift_ctx* ctx, int ticket, void* d_out, size_t cap,
@@ -1599,6 +1623,7 @@ const char* sift_hip_strerror(int status) {
         case SIFT_ERR_PARAM: return "parameter outside the supported range";
         case SIFT_ERR_STATE: return "invalid call order (no such job / no previous detect / too many jobs in flight)";
         case SIFT_ERR_NO_COMM: return "RCCL unavailable or a collective failed";
+        case SIFT_ERR_PEER: return "another rank of the collective failed";
         default: return "unknown error";
     }
 }

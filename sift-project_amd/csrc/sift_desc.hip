@@ -1,15 +1,9 @@
 // sift_desc.hip — compute_descriptors + update_histogram +
 // convert_hist_to_desc (reference src/sift.cpp:541-682) on gfx950.
 //
-// Two kernel shapes share one sample walk (desc_walk) and two sample bodies:
-//  * k_descriptor_split<F64>: one record per 256-thread workgroup, the
-//    window's rows dealt to its four waves (default: desc_mode 0, F64);
-//  * k_descriptor_wave<F64>: one record per wavefront, four independent
-//    waves per workgroup (A/B: desc_mode 1 = f32 sample math, round 3's
-//    default; desc_mode 3 = f64 sample math);
-// desc_mode 2 = the split kernel with f32 sample math (A/B).
-// F64 is the reference's arithmetic: every per-sample operation in double
-// (sift.cpp:641-678); f32 sample math moves the normalised floats by ~1e-7.
+// k_descriptor_split: one record per 256-thread workgroup, the window's
+// rows dealt to its four waves; every per-sample operation in double, as the
+// reference (sift.cpp:641-678), into f64 histograms.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -19,7 +13,7 @@
 #include "sift_math64.h"
 
 // replicas of the 4x4x8 f64 histogram per wave (power of two <= 16) and the
-// minimum workgroups per CU, per kernel shape
+// minimum workgroups per CU
 #ifndef SIFT_DSPLIT_REPS
 #define SIFT_DSPLIT_REPS 8
 #endif
@@ -28,12 +22,6 @@
 #endif
 #ifndef SIFT_DESC_AHEAD  // steps of 64 samples whose gradient loads are in flight
 #define SIFT_DESC_AHEAD 1
-#endif
-#ifndef SIFT_DESCW_REPS  // 16: conflict-free atomics; 4 / 8 measured equal on the bench
-#define SIFT_DESCW_REPS 16
-#endif
-#ifndef SIFT_DESCW_OCC
-#define SIFT_DESCW_OCC (SIFT_DESCW_REPS >= 16 ? 2 : 5)
 #endif
 
 namespace sift_amd {
@@ -55,13 +43,12 @@ struct DescRecord {
     RecSide side;
     const double* img;
     int W, H, x, y, radius;
-    double hw, ihw, sa, ca;      // hist_width, 1 / hist_width, sin / cos (F64)
-    float saf, caf, ihwf, porif, limf;
+    double hw, ihw, sa, ca;  // hist_width, 1 / hist_width, sin / cos of pori
+    float saf, caf, limf;    // f32 copies for the window bounds
 };
 
-// sa / ca: the f64 sin / cos of pori when the caller already has them
-// (F64, split kernel: computed once per record); otherwise computed here
-template <bool F64>
+// sa / ca: the f64 sin / cos of pori, computed once per record by the
+// kernel (sc)
 __device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevParams& P,
                                                   const sift_kp& R, const RecSide& side,
                                                   const double2* sc) {
@@ -84,23 +71,10 @@ __device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevP
     const double diag = sqrt((double)(d.W * d.W + d.H * d.H));
     d.radius = (int)((diag < rr) ? diag : rr);  // std::min(rr, diag)
     d.ihw = 1.0 / d.hw;
-    d.sa = 0.0;
-    d.ca = 1.0;
-    if (F64) {
-        if (sc) {
-            d.sa = sc->x;
-            d.ca = sc->y;
-        } else {
-            d.sa = sin(d.pori);
-            d.ca = cos(d.pori);
-        }
-        d.saf = (float)d.sa;
-        d.caf = (float)d.ca;
-    } else {
-        sincosf((float)d.pori, &d.saf, &d.caf);
-    }
-    d.ihwf = (float)d.ihw;
-    d.porif = (float)d.pori;
+    d.sa = sc->x;
+    d.ca = sc->y;
+    d.saf = (float)d.sa;
+    d.caf = (float)d.ca;
     d.limf = (float)((0.5 * kDescW + 0.5) * d.hw);  // |row_rot|, |col_rot| < 2.5 hw
     return d;
 }
@@ -108,7 +82,7 @@ __device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevP
 // ---------------------------------------------------------------------------
 // One sample (col, row) with gradient loads cv = I(x+1), I(x-1), I(y-1),
 // I(y+1) into this lane's replica `rep` (bin i at rep[i * NR]).
-// F64: the reference's expressions (sift.cpp:641-678): row_rot / col_rot
+// The reference's expressions (sift.cpp:641-678): row_rot / col_rot
 // with the correctly rounded division by hist_width, (row_rot + 2) - 0.5,
 // sqrt, atan2 - pori and the two fmods (exact compare-and-subtract),
 // exp(-(row_rot^2 + col_rot^2) / 8), the trilinear split of
@@ -167,44 +141,6 @@ __device__ __forceinline__ void add_sample_f64(double* rep, int scol, int srow, 
     }
 }
 
-// f32 sample math (A/B): rotated bin position, magnitude, atan2, exp2 and
-// the trilinear split in f32, histograms in f64
-template <int NR>
-__device__ __forceinline__ void add_sample_f32(double* rep, int scol, int srow, const double* cv,
-                                               const DescRecord& d) {
-    constexpr float kHalfW = (float)(kDescW / 2 - 0.5);
-    const float wscale = (float)(-1.4426950408889634 / (0.5 * kDescW * kDescW));
-    const float fcol = (float)scol, frow = (float)srow;
-    const float row_rot = fmaf(fcol, d.saf, frow * d.caf) * d.ihwf;
-    const float col_rot = fmaf(fcol, d.caf, -(frow * d.saf)) * d.ihwf;
-    const float rb = row_rot + kHalfW;
-    const float cb = col_rot + kHalfW;
-    const float dx = (float)(cv[0] - cv[1]);
-    const float dy = (float)(cv[2] - cv[3]);
-    const float mag = __builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy));
-    const float ob = (atan2_f32(dy, dx) - d.porif) * (float)(kDescBins / kTwoPi);
-    const float wgt = __builtin_amdgcn_exp2f(fmaf(row_rot, row_rot, col_rot * col_rot) * wscale);
-    const float m = mag * wgt;
-    const float fbr = floorf(rb), fbc = floorf(cb), fbo = floorf(ob);
-    const int br = (int)fbr, bc = (int)fbc, bo = (int)fbo;
-    const float fr = rb - fbr, fc = cb - fbc, fo = ob - fbo;
-#pragma unroll
-    for (int rq = 0; rq <= 1; ++rq) {
-        const int ri = br + rq;
-        if ((unsigned)ri >= (unsigned)kDescW) continue;
-        const float vr = m * ((rq == 0) ? 1.0f - fr : fr);
-#pragma unroll
-        for (int cq = 0; cq <= 1; ++cq) {
-            const int ci = bc + cq;
-            if ((unsigned)ci >= (unsigned)kDescW) continue;
-            const float vc = vr * ((cq == 0) ? 1.0f - fc : fc);
-            double* hb = &rep[(ri * 32 + ci * 8) * NR];
-            atomicAdd(&hb[(bo & 7) * NR], (double)(vc * (1.0f - fo)));
-            atomicAdd(&hb[((bo + 1) & 7) * NR], (double)(vc * fo));
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // The samples of rows j0, j0 + dj, ... of the window (row j = row - radius),
 // 64 rows per group (lane = row), walked 64 samples per step:
@@ -220,7 +156,7 @@ __device__ __forceinline__ void add_sample_f32(double* rep, int scol, int srow, 
 //    unconditionally: lanes past the end read pixel (1, 1), so the compiler
 //    can count them).
 // ---------------------------------------------------------------------------
-template <bool F64, int NR>
+template <int NR>
 __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, double* rep,
                                           const double2* atab, const double* gtab) {
     const int lane = threadIdx.x & 63;
@@ -297,10 +233,7 @@ __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, d
             qrow[A] = qcol[A] = 0;
             qok[A] = t0 + 64 * A < total && locate(t0 + 64 * A, qrow[A], qcol[A]);
             fetch(qok[A], qrow[A], qcol[A], qv[A]);
-            if (qok[0]) {
-                if (F64) add_sample_f64<NR>(rep, qcol[0], qrow[0], qv[0], d, atab, gtab);
-                else add_sample_f32<NR>(rep, qcol[0], qrow[0], qv[0], d);
-            }
+            if (qok[0]) add_sample_f64<NR>(rep, qcol[0], qrow[0], qv[0], d, atab, gtab);
 #pragma unroll
             for (int a = 0; a < A; ++a) {
                 qrow[a] = qrow[a + 1];
@@ -370,8 +303,7 @@ __device__ __forceinline__ void finish_record(double v0, double v1, const DescRe
 }
 
 // ---------------------------------------------------------------------------
-// k_descriptor_split<F64> (desc_mode 0 with F64, the default): one record
-// per 256-thread workgroup.
+// k_descriptor_split: one record per 256-thread workgroup.
 //  * Row j of the window goes to wave j % 4 (desc_walk with dj = 4), so a
 //    record takes a quarter of a wavefront's serial walk, and the split
 //    depends only on the record: its bytes do not depend on how its job
@@ -388,14 +320,12 @@ __device__ __forceinline__ void finish_record(double v0, double v1, const DescRe
 //    record.
 // ---------------------------------------------------------------------------
 constexpr int kSplitReps = SIFT_DSPLIT_REPS;
-// Gaussian weight table G(0..radius) of the current record (split kernel,
-// F64): one exp per thread per record instead of one per sample; records
+// Gaussian weight table G(0..radius) of the current record: one exp per thread per record instead of one per sample; records
 // with a larger radius evaluate exp per sample
 constexpr int kGTab = 256;
 static_assert(kSplitReps >= 1 && kSplitReps <= 16 && (kSplitReps & (kSplitReps - 1)) == 0,
               "replicas: a power of two <= 16");
 
-template <bool F64>
 __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     const PyrTable* __restrict__ pt, DevParams P, sift_kp* __restrict__ recs,
     const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
@@ -404,7 +334,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kSplitReps];
     __shared__ double2 atab[17];
     __shared__ unsigned next_k;
-    __shared__ double2 next_sc;  // sin, cos of the next record's pori (F64)
+    __shared__ double2 next_sc;  // sin, cos of the next record's pori
     __shared__ double gtab[kGTab];
     set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;
@@ -426,7 +356,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     // static striding throughout measured slower: no dynamic balance)
     auto prepare = [&](unsigned c) {
         next_k = c;
-        if (F64 && k0 + c < n) {
+        if (k0 + c < n) {
             const double pr = recs[k0 + c].pori;
             next_sc = make_double2(sin(pr), cos(pr));
         }
@@ -438,17 +368,16 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
         const unsigned k = k0 + cur;
         if (k >= n) break;
         const double2 sc = next_sc;
-        const DescRecord d = load_record<F64>(pt, P, recs[k], rec_side[k], &sc);
-        const bool use_tab = F64 && d.radius < kGTab;
+        const DescRecord d = load_record(pt, P, recs[k], rec_side[k], &sc);
+        const bool use_tab = d.radius < kGTab;
         if (use_tab && (int)threadIdx.x <= d.radius) {
             const double i = (double)threadIdx.x;
             gtab[threadIdx.x] = exp_f64(-(i * i) / (0.5 * kDescW * kDescW * d.hw * d.hw));
         }
         for (int i = lane; i < 64 * kSplitReps; i += 64)
             reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
-        if (F64) __syncthreads();  // the table (uniform: every thread gets here)
-        else wave_sync();
-        desc_walk<F64, kSplitReps>(d, wv, 4, rep, atab, use_tab ? gtab : nullptr);
+        __syncthreads();  // the table (uniform: every thread gets here)
+        desc_walk<kSplitReps>(d, wv, 4, rep, atab, use_tab ? gtab : nullptr);
         wave_sync();
         double v0, v1;
         reduce_replicas<kSplitReps>(hist, v0, v1);
@@ -470,77 +399,17 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_descriptor_wave<F64> (A/B: desc_mode 1 f32, 3 f64): one WAVEFRONT per
-// record, four independent waves per workgroup (wave g's first record is g,
-// then the work counter); no workgroup barrier anywhere (a
-// wave's LDS instructions execute in order, so zeroing -> accumulation ->
-// reduction -> next record's zeroing needs only compiler ordering,
-// wave_sync). A record's samples are one wave's serial walk.
-// ---------------------------------------------------------------------------
-constexpr int kDescWReps = SIFT_DESCW_REPS;
-static_assert(kDescWReps >= 1 && kDescWReps <= 16 && (kDescWReps & (kDescWReps - 1)) == 0,
-              "replicas: a power of two <= 16");
-
-template <bool F64>
-__global__ __launch_bounds__(256, SIFT_DESCW_OCC) void k_descriptor_wave(
-    const PyrTable* __restrict__ pt, DevParams P, sift_kp* __restrict__ recs,
-    const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
-    const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
-    unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kDescWReps];
-    __shared__ double2 atab[17];
-    set_job_prio(pt->jp, 0);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double* const hist = hist_all + wv * 128 * kDescWReps;
-    double* const rep = hist + (lane & (kDescWReps - 1));
-    const unsigned n = min(*n_rec, cap_rec);
-    const unsigned k0 = min(*rec_begin, n);
-    if (ex.cnt && blockIdx.x == 0 && threadIdx.x == 0) {
-        ex.cnt[0] = k0;
-        ex.cnt[1] = n;
-    }
-    if (F64) {
-        if (threadIdx.x < 17) atab[threadIdx.x] = kAtanTab[threadIdx.x];
-        __syncthreads();  // the only barrier, before any wave can leave
-    }
-    const unsigned n_waves = gridDim.x * 4;
-    for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n;) {  // first static, as split
-        const DescRecord d = load_record<F64>(pt, P, recs[k], rec_side[k], nullptr);
-        for (int i = lane; i < 64 * kDescWReps; i += 64)
-            reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
-        wave_sync();
-        desc_walk<F64, kDescWReps>(d, 0, 1, rep, atab, nullptr);
-        wave_sync();
-        double v0, v1;
-        reduce_replicas<kDescWReps>(hist, v0, v1);
-        finish_record(v0, v1, d, k, recs, desc_f32, ex);
-        wave_sync();
-        unsigned claim = 0;
-        if (lane == 0) claim = atomicAdd(work, 1u);
-        k = k0 + n_waves + __builtin_amdgcn_readfirstlane(claim);
-    }
-}
-
 }  // namespace
 
 hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* recs,
                              const RecSide* rec_side, const unsigned* rec_begin,
                              const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
-                             unsigned* work, const ExportSink& ex, unsigned wgs,
-                             int mode, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    // persistent grids: workgroups pull records
-    if (mode == 1 || mode == 3) {  // a record per wave, four waves per workgroup
-        const unsigned blocks = std::min<unsigned>(wgs, cap_rec > 0 ? (cap_rec + 3) / 4 : 1);
-        auto kern = mode == 3 ? k_descriptor_wave<true> : k_descriptor_wave<false>;
-        return launch_timed(kern, dim3(blocks), dim3(256), 0, s, e0, e1, d_pt, P, recs, rec_side,
-                            rec_begin, n_rec, cap_rec, desc_f32, work, ex);
-    }
+                             unsigned* work, const ExportSink& ex, unsigned wgs, hipStream_t s,
+                             hipEvent_t e0, hipEvent_t e1) {
+    // persistent grid: workgroups pull records
     const unsigned blocks = std::min<unsigned>(wgs, cap_rec > 0 ? cap_rec : 1);
-    auto kern = mode == 2 ? k_descriptor_split<false> : k_descriptor_split<true>;
-    return launch_timed(kern, dim3(blocks), dim3(256), 0, s, e0, e1, d_pt, P, recs, rec_side,
-                        rec_begin, n_rec, cap_rec, desc_f32, work, ex);
+    return launch_timed(k_descriptor_split, dim3(blocks), dim3(256), 0, s, e0, e1, d_pt, P, recs,
+                        rec_side, rec_begin, n_rec, cap_rec, desc_f32, work, ex);
 }
 
 }  // namespace sift_amd

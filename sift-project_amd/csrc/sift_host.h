@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstddef>
+#include <functional>
 #include <vector>
 
 #include "sift_types.h"
@@ -60,5 +61,9 @@ size_t host_finalize(const sift_params* p, sift_kp* recs, const RecSide* side, u
 // is what an stb-decoded Image holds (image_io.cpp:20-35); returns false
 // (dst unspecified) otherwise.
 bool host_pack_u8(const double* src, size_t n, uint8_t* dst);
+
+// fn(t) for t in [0, n_tasks) on the same persistent host threads (the
+// caller included); returns when all are done
+void host_parallel(unsigned n_tasks, const std::function<void(unsigned)>& fn);
 
 }  // namespace sift_amd

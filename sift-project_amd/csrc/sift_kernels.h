@@ -75,8 +75,7 @@ hipError_t launch_descriptor(const PyrTable* d_pt, const DevParams& P, sift_kp* 
                              const RecSide* rec_side, const unsigned* rec_begin,
                              const unsigned* n_rec, unsigned cap_rec, float* desc_f32,
                              unsigned* work, const ExportSink& ex, unsigned wgs,
-                             int mode, hipStream_t s, hipEvent_t e0 = nullptr,
-                             hipEvent_t e1 = nullptr);
+                             hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // out[i] = recs[items[i].src] with size = items[i].size (final records on the device)
 hipError_t launch_gather_records(const sift_kp* recs, const GatherItem* items, unsigned n,

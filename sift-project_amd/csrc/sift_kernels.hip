@@ -53,15 +53,6 @@
 #ifndef SIFT_ORI_AHEAD  // k_orient_wave: steps of 64 samples whose loads are in flight
 #define SIFT_ORI_AHEAD 1
 #endif
-// SIFT_LAB_ORI: attribution builds only (make alt; wrong results): 1 no
-// histogram atomics, 2 no sqrt / atan2, 3 no smoothing, 4 no window sweep,
-// 5 claims only, 6 no sweep and no weight table
-#ifndef SIFT_LAB_ORI
-#define SIFT_LAB_ORI 0
-#endif
-#ifndef SIFT_ORI_FAST  // k_orient_wave: sqrt_f64 + atan2_f32 (0: ocml sqrt + atan2f, A/B)
-#define SIFT_ORI_FAST 1
-#endif
 #ifndef SIFT_EXT_PF
 #define SIFT_EXT_PF 2  // k_extrema_stream: rows in flight
 #endif
@@ -1190,6 +1181,12 @@ __host__ __device__ constexpr int ori_wave_lds_doubles(int nb) {
     return kOriWReps * nb + kOriWTab + (nb > 64 ? nb : 0) + 2 * kOriEmit;
 }
 
+// the rare exact-bin path (f64 atan2, sift.cpp:489), out of line so its
+// registers do not count against the sample loop's
+__device__ __noinline__ int ori_bin_exact(double dy, double dx, int nb) {
+    return (int)round(nb * (atan2(dy, dx) + kPi) / kTwoPi);
+}
+
 __global__ __launch_bounds__(256, 4) void k_orient_wave(
     const PyrTable* __restrict__ pt, DevParams P, const RawKp* __restrict__ raw,
     const unsigned* __restrict__ raw_begin, const unsigned* __restrict__ n_raw, unsigned cap_raw,
@@ -1251,10 +1248,6 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
     // fewer waves, ~9 keypoints each, the dynamic balance wins by 1 %)
     const unsigned n_waves = gridDim.x * 4;
     for (unsigned k = k0 + blockIdx.x * 4 + wv; k < n;) {
-        if (SIFT_LAB_ORI == 5) {
-            k = n;
-            continue;
-        }
         const RawKp kp = raw[k];
         const int o = kp.octave;
         const double inv = 1.0 / pow2i(o);
@@ -1269,7 +1262,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
         const int kmax = 2 * radius * radius;
         const bool use_tab = kmax < kOriWTab;
         for (int i = lane; i < kOriWReps * nb; i += 64) hist[i] = 0.0;
-        if (use_tab && SIFT_LAB_ORI != 6)
+        if (use_tab)
             for (int q = lane; q <= kmax; q += 64) wtab[q] = exp(-q / denom);
         wave_sync();
         // the side x side window flattened, 64 samples per step; sample s
@@ -1309,9 +1302,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
             qok[a] = fetch(64 * a + lane, pi_, pj_, qv[a]);
             advance(pi_, pj_);
         }
-        double lab_acc = 0.0;  // SIFT_LAB_ORI attribution builds only
-        (void)lab_acc;
-        for (int s0 = 0; s0 < (SIFT_LAB_ORI >= 4 ? 0 : nsamp); s0 += 64) {
+        for (int s0 = 0; s0 < nsamp; s0 += 64) {
             qi[A] = pi_;
             qj[A] = pj_;
             qok[A] = fetch(s0 + 64 * A + lane, pi_, pj_, qv[A]);
@@ -1322,29 +1313,17 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
                 cj_ = qj[0];
                 const double dx = cv[0] - cv[1];
                 const double dy = cv[2] - cv[3];
-#if SIFT_LAB_ORI == 2
-                const double mag = dx * dx + dy * dy;
-                const float at = (float)dx;
-#elif SIFT_ORI_FAST
                 const double mag = sqrt_f64(dx * dx + dy * dy);  // correctly rounded
                 const float at = atan2_f32((float)dy, (float)dx);
-#else
-                const double mag = sqrt(dx * dx + dy * dy);
-                const float at = atan2f((float)dy, (float)dx);
-#endif
                 const int k2 = ci_ * ci_ + cj_ * cj_;
                 const double wgt = use_tab ? wtab[k2] : exp(-k2 / denom);
                 const float t = nbf * (at + (float)kPi) * (float)(1.0 / kTwoPi);
                 int hidx = (int)rintf(t);
                 const bool tiny = (dx != 0.0 && fabs(dx) < 1e-30) || (dy != 0.0 && fabs(dy) < 1e-30);
                 if (fabs((double)t - floor((double)t) - 0.5) < bin_guard || tiny)
-                    hidx = (int)round(nb * (atan2(dy, dx) + kPi) / kTwoPi);  // exact path
+                    hidx = ori_bin_exact(dy, dx, nb);  // exact path
                 hidx = (hidx < nb) ? hidx : 0;
-#if SIFT_LAB_ORI == 1
-                lab_acc += wgt * mag + hidx;
-#else
                 atomicAdd(&rep[hidx * kOriWReps], wgt * mag);
-#endif
             }
 #pragma unroll
             for (int a = 0; a < A; ++a) {
@@ -1355,9 +1334,6 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
                 for (int q = 0; q < 4; ++q) qv[a][q] = qv[a + 1][q];
             }
         }
-#if SIFT_LAB_ORI == 1
-        if (lab_acc == 1234.5) hist[lane] = lab_acc;
-#endif
         wave_sync();
         // smoothing (sift.cpp:496-504) and peaks (sift.cpp:507-531)
         auto emit = [&](bool peak, double ori) {  // into the wave's buffer
@@ -1386,7 +1362,7 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
 #pragma unroll
                 for (int q = 0; q < kOriWReps; ++q)
                     h += hist[lane * kOriWReps + ((q + lane) & (kOriWReps - 1))];
-            for (int it = 0; it < (SIFT_LAB_ORI == 3 ? 0 : kSmoothIters); ++it) {
+            for (int it = 0; it < kSmoothIters; ++it) {
                 const double hn = __shfl(h, lane + 1 < nb ? lane + 1 : 0);  // old h[i+1]
                 const double c = 0.5 * h, d = 0.25 * hn;
                 double prev = readlane_f64(h, nb - 1);  // h[i-1] for i = 0: old
@@ -1696,11 +1672,14 @@ __global__ __launch_bounds__(256) void k_gather_records(const sift_kp* __restric
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
     __syncthreads();
     if (threadIdx.x == 0) {
-        atomicAdd(acc, part[0] + part[1] + part[2] + part[3]);
-        // the add has returned (performed at the device coherence point)
-        // before the done increment is issued
-        __builtin_amdgcn_s_waitcnt(0);
-        if (atomicAdd(done, 1u) == gridDim.x - 1) *checksum = atomicAdd(acc, 0ull);
+        // the partial sum is published by the acq_rel done increment
+        // (release); the last workgroup's increment also acquires every
+        // other workgroup's add before it reads the total
+        __hip_atomic_fetch_add(acc, part[0] + part[1] + part[2] + part[3], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            gridDim.x - 1)
+            *checksum = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1759,10 +1738,14 @@ __global__ __launch_bounds__(256) void k_verify_slots(const unsigned long long* 
     if (threadIdx.x != 0) return;
     unsigned long long* acc = scratch + 2 * slot;
     unsigned long long* done = acc + 1;
-    atomicAdd(acc, part[0] + part[1] + part[2] + part[3]);
-    __builtin_amdgcn_s_waitcnt(0);  // the add has returned before the done count
-    if (atomicAdd(done, 1ull) != gridDim.x - 1) return;
-    const unsigned long long total = atomicAdd(acc, 0ull);
+    // published by the acq_rel done count; the last workgroup acquires all
+    __hip_atomic_fetch_add(acc, part[0] + part[1] + part[2] + part[3], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(done, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) !=
+        gridDim.x - 1)
+        return;
+    const unsigned long long total = __hip_atomic_load(acc, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long want = 0;
     for (int k = 0; k < n_sums; ++k) want += sl[sum_word + k];
     if (n > cap_rows || total != want) atomicAdd(bad, 1ull);

@@ -71,7 +71,13 @@ __device__ __forceinline__ double atan2_f64(double y, double x, const double2* t
     const double ax = fabs(x), ay = fabs(y);
     const bool swap = ay > ax;
     const double mx = swap ? ay : ax, mn = swap ? ax : ay;
-    const float af = (float)mn * __builtin_amdgcn_rcpf((float)mx);
+    // table point from an f32 estimate of mn/mx, both operands first scaled
+    // by the same power of two (exact) so that tiny or subnormal gradients do
+    // not leave the f32 range: a flushed mx would give inf / NaN and push kf
+    // to 16, where |u| reaches 1, outside the series' range
+    const int ex = __builtin_amdgcn_frexp_exp(mx);
+    const float af = (float)__builtin_ldexp(mn, -ex) *
+                     __builtin_amdgcn_rcpf((float)__builtin_ldexp(mx, -ex));
     const float kf = __builtin_rintf(fminf(fmaxf(af * 16.0f, 0.0f), 16.0f));
     const double c = (double)kf * 0.0625;
     const double num = __builtin_fma(-c, mx, mn);

@@ -211,3 +211,45 @@ def test_record_exchange_bucketed_gloo():
             for i in shard(2 * world, rr, world):
                 assert got[i] == _records(2, i, 5 + 2 + rr).tobytes()
                 assert last[i] == _records(3, i, 5 + 3 + rr).tobytes()
+
+
+def test_native_exchange_protocol_multirank():
+    """The protocol sift_hip_allgather_records runs over RCCL
+    (csrc/sift_exchange.h) at world sizes 1-4 on host threads with a
+    host-memory transport (tools/exchange_selftest.cpp): padding to the
+    largest rank, slot offsets and the rank-major compaction with uneven and
+    empty ranks, and injected local failures (bad argument, max_local
+    mismatch, allocation / staging failure, too-small output) after which
+    every rank returns with the agreed status and none is left in a
+    collective (a hang exits 3 via the watchdog)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                       "exchange_selftest")
+    if not os.path.exists(exe):
+        pytest.skip("tools/exchange_selftest not built (run __graft_entry__.build())")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ALL OK" in r.stdout
+    assert r.stdout.count("\nok ") + r.stdout.startswith("ok ") >= 10
+
+
+def test_bench_gpus_n_launches_one_worker_per_gpu():
+    """`bench.py --gpus 2` without a launcher starts torch.distributed.run
+    with two workers itself (it never measures one GPU under --gpus N); here,
+    without GPUs, the workers fail and the exit status says so. A WORLD_SIZE
+    that disagrees with --gpus is an error, not a warning."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
+                        "1", "--warmup", "1"], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert "torch.distributed.run" in r.stderr and "--nproc-per-node=2" in r.stderr
+    if not torch.cuda.is_available():
+        assert r.returncode != 0 and r.stdout.strip() == ""
+    env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r2 = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                        capture_output=True, text=True, timeout=300, env=env2)
+    assert r2.returncode == 2 and "WORLD_SIZE=1" in r2.stderr

@@ -262,12 +262,9 @@ def test_gpu_pyramid_paths_match_oracle(lds_px, shape):
         ctx.close()
 
 
-# Descriptor variants (SIFT_DESC_MODE): 0 = k_descriptor_split with f64
-# sample math (default), 1 = k_descriptor_wave (a wavefront per record, f32
-# sample math), 2 = k_descriptor_split with f32 sample math, 3 = k_descriptor_wave
-# with f64 sample math. Each must meet
-# the descriptor contract on the 1080p golden and on the stb-decoded
-# photographs (natural gradients).
+# The descriptor (k_descriptor_split, every per-sample operation in f64)
+# against the 1080p golden and the stb-decoded photographs (natural
+# gradients).
 DESC_GOLDENS = [g for g in GOLDENS if g.name in ("synth_1920x1080", "image1",
                                                  "photo_cave01_00")]
 
@@ -282,23 +279,3 @@ def test_gpu_descriptor_f64_reference_precision(gpu_ctx, g):
     print(g.name, r)
     assert final_ok(r), r
     assert r["desc_u8_mismatch"] == 0 and r["desc_f32_max"] <= DESC_F64_F32_TOL, r
-
-
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
-@pytest.mark.parametrize("g", DESC_GOLDENS, ids=[g.name for g in DESC_GOLDENS])
-def test_gpu_descriptor_modes_match_golden(mode, g):
-    import os
-
-    from sift_hip import Context
-
-    os.environ["SIFT_DESC_MODE"] = mode
-    try:
-        ctx = Context(0)
-    finally:
-        del os.environ["SIFT_DESC_MODE"]
-    try:
-        kps, df = ctx.detect(g.input(), g.params(), desc_f32=True)
-        r = compare_final(kps, df, g.final, g.desc_f32)
-        assert final_ok(r), r
-    finally:
-        ctx.close()

@@ -67,6 +67,38 @@ for step in "$@"; do
         --no-alone --no-big --no-extra --step-log > $O/steplog.json 2> $O/steplog.err \
         || { tail -20 $O/steplog.err; exit 1; }
     grep -A70 "step log" $O/steplog.err ;;
+  big)
+    # BASELINE configs 3 and 5: job timeline with host phases (untraced),
+    # rocprofv3 kernel trace of the pipelined leg (2 jobs in flight) and of
+    # a serialised context (kernels alone); $BIG_CONFIGS, $BIG_IMAGES
+    for cfg in ${BIG_CONFIGS:-config3 config5}; do
+      timeout -k 10 300 python3 tools/big_profile.py $cfg --images ${BIG_IMAGES:-12} \
+          > $O/big_$cfg.json 2> $O/big_$cfg.err || { tail -20 $O/big_$cfg.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/big_$cfg.json')); print('$cfg', d['ms_per_image'], d['keypoints_per_image'])"
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $R/$O/b_$cfg -o run \
+          -- python3 $R/tools/big_profile.py $cfg --images ${BIG_IMAGES:-12} \
+          > $R/$O/big_prof_$cfg.json 2> $R/$O/big_prof_$cfg.err \
+          || { tail -20 $R/$O/big_prof_$cfg.err; exit 1; }
+      SIFT_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $R/$O/bs_$cfg -o run \
+          -- python3 $R/tools/big_profile.py $cfg --images 4 --sync \
+          > $R/$O/big_ser_$cfg.json 2> $R/$O/big_ser_$cfg.err \
+          || { tail -20 $R/$O/big_ser_$cfg.err; exit 1; }
+      cd $R
+      python tools/prof_summary.py $O/b_$cfg/run_kernel_trace.csv > $O/summary_$cfg.txt
+      python tools/prof_summary.py $O/bs_$cfg/run_kernel_trace.csv > $O/summary_serial_$cfg.txt
+      python tools/prof_timeline.py $O/b_$cfg/run_kernel_trace.csv > $O/timeline_$cfg.txt
+      rm -rf $O/b_$cfg $O/bs_$cfg
+    done
+    echo BIG_DONE ;;
+  bigdepth)
+    # the BASELINE config 3 / 5 legs at 2 and 3 jobs in flight (bench.py legs only)
+    for d in 2 3; do
+      SIFT_BIG_DEPTH=$d timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-extra \
+          --no-alone --no-cpu-baseline --no-matcher > $O/bigdepth_$d.json 2> $O/bigdepth_$d.err \
+          || { tail -20 $O/bigdepth_$d.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/bigdepth_$d.json')); print('depth $d', [(c, round(d[c]['ms_per_image'],3), d[c]['host_phases_ms']) for c in ('config3','config5')])"
+    done ;;
   divcheck)
     timeout -k 10 300 tools/divcheck > $O/divcheck.txt 2>&1 || { tail -5 $O/divcheck.txt; exit 1; }
     tail -3 $O/divcheck.txt ;;

@@ -96,6 +96,11 @@ int main(int argc, char** argv) {
                 const double k = (double)(next_u64() % 17) / 16.0;
                 y = x * k * (1.0 + (uni() - 0.5) * 1e-6);
             }
+            if (fn == 1 && kind == 8) {  // below the f32 range, and subnormal
+                const double s = (next_u64() & 1) ? 0x1p-700 : 0x1p-1040;
+                x *= s;
+                y *= s;
+            }
             a[i] = y;
             b[i] = x;
         }

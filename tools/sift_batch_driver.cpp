@@ -122,11 +122,20 @@ int exchange(Rank& r, sift_comm* comm, int max_local, int n_ranks) {
                                         nullptr);
     if (st != SIFT_OK && st != SIFT_ERR_ARG) return st;
     r.cap_all = r.n_all;
-    if (hipMalloc(&r.d_all, std::max<size_t>(r.cap_all, 1) * sizeof(sift_kp)) != hipSuccess)
-        return SIFT_ERR_NOMEM;
-    CHECK(sift_hip_allgather_records(comm, r.d_recs, r.ids.data(), r.counts.data(),
-                                     (int)r.ids.size(), max_local, r.d_all, r.cap_all,
-                                     r.all_ids.data(), r.all_counts.data(), &r.n_all, nullptr));
+    // an allocation failure still joins the second exchange (with no output
+    // room: it returns SIFT_ERR_ARG once the collectives are done), so no
+    // peer is left waiting in it
+    int alloc = SIFT_OK;
+    if (hipMalloc(&r.d_all, std::max<size_t>(r.cap_all, 1) * sizeof(sift_kp)) != hipSuccess) {
+        r.d_all = nullptr;
+        r.cap_all = 0;
+        alloc = SIFT_ERR_NOMEM;
+    }
+    st = sift_hip_allgather_records(comm, r.d_recs, r.ids.data(), r.counts.data(),
+                                    (int)r.ids.size(), max_local, r.d_all, r.cap_all,
+                                    r.all_ids.data(), r.all_counts.data(), &r.n_all, nullptr);
+    if (alloc != SIFT_OK) return alloc;
+    CHECK(st);
     r.ms_exchange = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     return SIFT_OK;
 }
