@@ -70,14 +70,15 @@ __device__ __forceinline__ double sqrt_f64(double s) {
 __device__ __forceinline__ double atan2_f64(double y, double x, const double2* tab) {
     const double ax = fabs(x), ay = fabs(y);
     const bool swap = ay > ax;
-    const double mx = swap ? ay : ax, mn = swap ? ax : ay;
-    // table point from an f32 estimate of mn/mx, both operands first scaled
-    // by the same power of two (exact) so that tiny or subnormal gradients do
-    // not leave the f32 range: a flushed mx would give inf / NaN and push kf
-    // to 16, where |u| reaches 1, outside the series' range
-    const int ex = __builtin_amdgcn_frexp_exp(mx);
-    const float af = (float)__builtin_ldexp(mn, -ex) *
-                     __builtin_amdgcn_rcpf((float)__builtin_ldexp(mx, -ex));
+    // both operands scaled by the same power of two so that mx is in [0.5, 1):
+    // exact, and the ratio and every step below are unchanged for normal
+    // operands, while tiny or subnormal gradients stay in range for the f32
+    // estimate (a flushed mx gave inf / NaN and pushed kf to 16, where |u|
+    // reaches 1, outside the series' range) and for the f64 reciprocal
+    const int ex = __builtin_amdgcn_frexp_exp(swap ? ay : ax);
+    const double mx = __builtin_ldexp(swap ? ay : ax, -ex);
+    const double mn = __builtin_ldexp(swap ? ax : ay, -ex);
+    const float af = (float)mn * __builtin_amdgcn_rcpf((float)mx);
     const float kf = __builtin_rintf(fminf(fmaxf(af * 16.0f, 0.0f), 16.0f));
     const double c = (double)kf * 0.0625;
     const double num = __builtin_fma(-c, mx, mn);
