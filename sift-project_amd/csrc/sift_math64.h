@@ -66,18 +66,20 @@ __device__ __forceinline__ double sqrt_f64(double s) {
     return s > 0.0 ? g : s;  // rsq(0) = inf
 }
 
+// atan2 for max(|x|, |y|) below the f32 normal range (never seen on image
+// gradients, but kept correct): ocml's f64 atan2, out of line so the common
+// path's registers do not pay for it
+__device__ __noinline__ double atan2_tiny(double y, double x) { return atan2(y, x); }
+
 // atan2(y, x); `tab` = kAtanTab staged in LDS
 __device__ __forceinline__ double atan2_f64(double y, double x, const double2* tab) {
     const double ax = fabs(x), ay = fabs(y);
     const bool swap = ay > ax;
-    // both operands scaled by the same power of two so that mx is in [0.5, 1):
-    // exact, and the ratio and every step below are unchanged for normal
-    // operands, while tiny or subnormal gradients stay in range for the f32
-    // estimate (a flushed mx gave inf / NaN and pushed kf to 16, where |u|
-    // reaches 1, outside the series' range) and for the f64 reciprocal
-    const int ex = __builtin_amdgcn_frexp_exp(swap ? ay : ax);
-    const double mx = __builtin_ldexp(swap ? ay : ax, -ex);
-    const double mn = __builtin_ldexp(swap ? ax : ay, -ex);
+    const double mx = swap ? ay : ax, mn = swap ? ax : ay;
+    // the table point comes from an f32 estimate of mn / mx: below FLT_MIN,
+    // (float)mx flushes (inf / NaN estimate, kf = 16, |u| up to 1: outside
+    // the series' range) and the f64 reciprocal below loses range too
+    if (mx < 0x1p-120 && mx > 0.0) return atan2_tiny(y, x);
     const float af = (float)mn * __builtin_amdgcn_rcpf((float)mx);
     const float kf = __builtin_rintf(fminf(fmaxf(af * 16.0f, 0.0f), 16.0f));
     const double c = (double)kf * 0.0625;
