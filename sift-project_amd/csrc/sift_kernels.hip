@@ -496,10 +496,13 @@ static_assert(kTileH == 4 * 8, "column pass: 256 threads = 64 columns x 4 runs o
 // live in LDS, so each level is two barrier-separated LDS sweeps instead of
 // a latency-bound launch; each finished level is streamed to its global
 // plane (needed later by extrema/orientation/descriptor), and the decimated
-// level `intervals` becomes the next octave's base in LDS (all three regions:
-// kLdsOctaveBytes). Same arithmetic and order as k_blur (image.cpp:156-214),
-// replicate borders by clamping. 16 waves sweep 16 rows x 64 columns at a
-// time; the radius is a template parameter so the taps sit in registers.
+// level `intervals` becomes the next octave's base in LDS. Same arithmetic
+// and order as k_blur (image.cpp:156-214), replicate borders by clamping.
+// Every level's taps, sum_w and 1/sum_w are staged in LDS once at the start
+// (a level used to load them from global memory inside its loops: a fixed
+// ~3,500-cycle cost per level that dominated the tiny octaves; stamped
+// copy in tools/lds_lab.hip, round 5); the radius is a template parameter,
+// so the taps of a level sit in registers.
 // ---------------------------------------------------------------------------
 struct LdsLevel {
     double* A;  // current level (in: previous level, out: this level), row stride P
@@ -511,23 +514,33 @@ struct LdsLevel {
     bool dec;
 };
 
-// One level: every thread takes runs of kLdsRun consecutive outputs (along
-// x in the row pass, along y in the column pass), loads the run plus its 2R
-// halo once from LDS and evaluates the kLdsRun independent dependency chains
-// interleaved (one output per thread was LDS- and latency-bound: 2R+1 reads
-// and one serial chain per output, on one CU). Row-pass tasks go lane-per-
-// row and the odd stride P keeps those lanes on different banks (a lane-per-
-// run mapping measured 6.7 bank-conflict cycles per LDS instruction).
-constexpr int kLdsRun = 8;
-constexpr int kLdsGenericPx = 600;
+// A level's output pixel: the plane in LDS and in global memory, and the
+// next octave's base (resize_inter_nearest, image.cpp:41-55) when due.
+__device__ __forceinline__ void lds_put(const LdsLevel& L, int x, int y, double o) {
+    L.A[y * L.P + x] = o;
+    L.g[y * L.W + x] = o;
+    if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
+        L.D[(y >> 1) * L.Pd + (x >> 1)] = o;
+        L.gd[(y >> 1) * L.Wd + (x >> 1)] = o;
+    }
+}
+
+// Levels of more than kLdsTinyPx pixels: every thread takes runs of kLdsRun
+// consecutive outputs (along x in the row pass, along y in the column pass),
+// loads the run plus its 2R halo once from LDS and evaluates the kLdsRun
+// independent dependency chains interleaved. Row-pass tasks go lane-per-row
+// and the odd stride P keeps those lanes on different banks. Runs of 4 (not
+// 8) put twice the waves on the level's FP64 work.
+constexpr int kLdsRun = 4;
+constexpr int kLdsTinyPx = 600;
 
 template <int R>
-__device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
+__device__ void lds_level(const LdsLevel& L, const double* __restrict__ tp) {
     constexpr int NV = kLdsRun + 2 * R;
     double k[R + 1];
 #pragma unroll
-    for (int u = 0; u <= R; ++u) k[u] = t.k[u];
-    const double sw = t.sum_w, inv = t.inv;
+    for (int u = 0; u <= R; ++u) k[u] = tp[u];
+    const double sw = tp[kMaxTemplR + 1], inv = tp[kMaxTemplR + 2];
     const int W = L.W, H = L.H, P = L.P;
     // row pass (image.cpp:170-185): task = (row y, run of columns from x0)
     const int rx = (W + kLdsRun - 1) / kLdsRun;
@@ -579,22 +592,43 @@ __device__ void lds_level(const LdsLevel& L, const BlurTaps& t) {
 #pragma unroll
             for (int j = 0; j < kLdsRun; ++j) acc[j] += k[u] * (v[j + R + u] + v[j + R - u]);
 #pragma unroll
-        for (int j = 0; j < kLdsRun; ++j) {
-            const int y = y0 + j;
-            if (y < H) {
-                const double o = div_sum_w(acc[j], sw, inv);
-                L.A[y * P + x] = o;
-                L.g[y * W + x] = o;
-                if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
-                    L.D[(y >> 1) * L.Pd + (x >> 1)] = o;
-                    L.gd[(y >> 1) * L.Wd + (x >> 1)] = o;
-                }
-            }
-        }
+        for (int j = 0; j < kLdsRun; ++j)
+            if (y0 + j < H) lds_put(L, x, y0 + j, div_sum_w(acc[j], sw, inv));
     }
     __syncthreads();
 }
 
+// Levels of at most kLdsTinyPx pixels (1080p: 30x16 and below): one output
+// per thread, a pass is a single short task per thread
+template <int R>
+__device__ void lds_level_tiny(const LdsLevel& L, const double* __restrict__ tp) {
+    double k[R + 1];
+#pragma unroll
+    for (int u = 0; u <= R; ++u) k[u] = tp[u];
+    const double sw = tp[kMaxTemplR + 1], inv = tp[kMaxTemplR + 2];
+    const int W = L.W, H = L.H, P = L.P;
+    for (int i = threadIdx.x; i < W * H; i += blockDim.x) {
+        const int y = i / W, x = i - y * W;
+        const double* row = L.A + y * P;
+        double acc = row[x] * k[0];
+#pragma unroll
+        for (int u = 1; u <= R; ++u) acc += k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
+        L.T[y * P + x] = div_sum_w(acc, sw, inv);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < W * H; i += blockDim.x) {
+        const int y = i / W, x = i - y * W;
+        double acc = L.T[y * P + x] * k[0];
+#pragma unroll
+        for (int u = 1; u <= R; ++u)
+            acc += k[u] * (L.T[min(y + u, H - 1) * P + x] + L.T[max(y - u, 0) * P + x]);
+        lds_put(L, x, y, div_sum_w(acc, sw, inv));
+    }
+    __syncthreads();
+}
+
+// kernels wider than kMaxTemplR (unusual sigmas): runtime radius, taps and
+// IEEE division from the global table
 __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int W = L.W, H = L.H, R = t.R, P = L.P;
@@ -612,13 +646,7 @@ __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
             double acc = L.T[y * P + x] * t.k[0];
             for (int u = 1; u <= R; ++u)
                 acc += t.k[u] * (L.T[min(y + u, H - 1) * P + x] + L.T[max(y - u, 0) * P + x]);
-            const double v = acc / t.sum_w;
-            L.A[y * P + x] = v;
-            L.g[y * W + x] = v;
-            if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
-                L.D[(y >> 1) * L.Pd + (x >> 1)] = v;
-                L.gd[(y >> 1) * L.Wd + (x >> 1)] = v;
-            }
+            lds_put(L, x, y, acc / t.sum_w);
         }
     }
     __syncthreads();
@@ -631,10 +659,22 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, nt = blockDim.x;
     const int dec_level = n_gauss - 3;
-    const int b = blockIdx.x;                // image of the job
-    double* A = lds;                         // current level
-    double* T = lds + kLdsOctavePx;          // horizontal-pass temporary
-    double* D = lds + 2 * kLdsOctavePx;      // next octave's base
+    const int b = blockIdx.x;                           // image of the job
+    // the level's plane lives in the large region A, the next octave's base
+    // in the quarter region D; the roles swap from octave to octave (the
+    // next octave's levels fit in the quarter region), so no copy
+    double* A = lds;                                    // current level
+    double* T = lds + kLdsOctavePx;                     // horizontal-pass temporary
+    double* D = lds + 2 * kLdsOctavePx;                 // next octave's base
+    double* const TP = lds + 2 * kLdsOctavePx + kLdsOctavePx / 4;  // staged taps
+    for (int i = tid; i < n_gauss * kLdsTapStride; i += nt) {
+        const int l = i / kLdsTapStride, j = i - l * kLdsTapStride;
+        const BlurTaps& t = taps[l];
+        double v = 0.0;
+        if (j <= kMaxTemplR) v = j <= t.R ? t.k[j] : 0.0;
+        else v = j == kMaxTemplR + 1 ? t.sum_w : t.inv;
+        TP[i] = v;
+    }
     {
         const int W = pt->w[o_first], H = pt->h[o_first], P = W | 1;
         const double* g0 = plane(pt, b, o_first, 0);
@@ -657,22 +697,16 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
         L.Hd = has_next ? pt->h[o + 1] : 0;
         L.Pd = L.Wd | 1;
         L.gd = has_next ? const_cast<double*>(plane(pt, b, o + 1, 0)) : nullptr;
+        const bool tiny = L.W * L.H <= kLdsTinyPx;
         for (int l = 1; l < n_gauss; ++l) {
             L.g = const_cast<double*>(plane(pt, b, o, l));
             L.dec = has_next && l == dec_level;
-            const BlurTaps& t = taps[l];
-            // the tiny octaves (<= 600 px: 30x16 and below at 1080p) with one
-            // output per thread and a runtime-radius loop: a pass there is
-            // one short task per thread, and the compact code beats the
-            // unrolled runs (76.7 vs 83.6 us for the whole launch alone)
-            if (L.W * L.H <= kLdsGenericPx) {
-                lds_level_any(L, t);
-                continue;
-            }
-            switch (t.R) {
-#define SIFT_LDS_CASE(RR) \
-    case RR:              \
-        lds_level<RR>(L, t); \
+            const double* tp = TP + l * kLdsTapStride;
+            switch (taps[l].R) {
+#define SIFT_LDS_CASE(RR)                                      \
+    case RR:                                                   \
+        if (tiny) lds_level_tiny<RR>(L, tp);                   \
+        else lds_level<RR>(L, tp);                             \
         break;
                 SIFT_LDS_CASE(1) SIFT_LDS_CASE(2) SIFT_LDS_CASE(3) SIFT_LDS_CASE(4)
                 SIFT_LDS_CASE(5) SIFT_LDS_CASE(6) SIFT_LDS_CASE(7) SIFT_LDS_CASE(8)
@@ -680,13 +714,13 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
                 SIFT_LDS_CASE(13) SIFT_LDS_CASE(14) SIFT_LDS_CASE(15) SIFT_LDS_CASE(16)
 #undef SIFT_LDS_CASE
                 default:
-                    lds_level_any(L, t);
+                    lds_level_any(L, taps[l]);
             }
         }
-        if (has_next) {  // next base becomes the current level (same stride Pd)
-            for (int i = tid; i < L.Pd * L.Hd; i += nt) A[i] = D[i];
-            __syncthreads();
-        }
+        // the next octave's base (row stride Pd) becomes the current level
+        double* t = A;
+        A = D;
+        D = t;
     }
 }
 
@@ -1500,8 +1534,9 @@ BlurShape blur_shape_for(int W, int H, int R) {
     b.cols = (!(W & 1) && px >= ((size_t)1 << 20)) ? 2 : 1;
     if (px >= ((size_t)4 << 20)) b.cols = std::min(b.cols, SIFT_BLUR_BIG_COLS);
     b.rows = px >= ((size_t)4 << 20) ? SIFT_BLUR_BIG_ROWS : 16;  // 48 / 64 / 96 rows measured slower;
-    // round 4: 24 / 48 / 64 rows for R >= 6 only: octave 0 alone within 1 %
-    if (R > 12 && b.cols == 2) b.rows = 16;
+    // round 4: 24 / 48 / 64 rows for R >= 6 only: octave 0 alone within 1 %;
+    // R > 12 (config 3's R = 14 level) also at 32 rows: 8192^2 alone 546 ->
+    // 415 us against the 16 rows it used to take (tools/blur_lab.hip, round 5)
     if (b.rows > H) b.rows = H;
     return b;
 }

@@ -29,13 +29,18 @@ constexpr int kMaxTemplR = 16;    // widest register-window blur kernel (the
 constexpr int kMaxTaps = 64;      // generic path: kernels up to 64 taps
 constexpr int kMaxBins = 256;     // orientation bins supported
 // octaves of at most this many pixels run LDS-resident: level + temporary +
-// quarter-size next base = 2.25 * 9088 * 8 B = 163,584 B of the 163,840 B LDS
-constexpr int kLdsOctavePx = 9088;
+// quarter-size next base + every level's staged taps (kMaxLevels x
+// kLdsTapStride doubles: k[0..kMaxTemplR], sum_w, 1/sum_w) =
+// (2.25 * 8960 + 228) * 8 B = 163,104 B of the 163,840 B LDS
+constexpr int kLdsOctavePx = 8960;
+constexpr int kLdsTapStride = kMaxTemplR + 3;
 // ... by default only octaves of at most this many pixels run there (1080p:
 // 60x33 and smaller; 120x67 as per-level tile launches on several CUs:
 // -2.5 % pipelined, 76 -> 23 + 48 us alone, round 4)
 constexpr int kLdsOctaveMaxPx = 2100;
-constexpr size_t kLdsOctaveBytes = (2 * (size_t)kLdsOctavePx + kLdsOctavePx / 4) * sizeof(double);
+constexpr size_t kLdsOctaveBytes =
+    (2 * (size_t)kLdsOctavePx + kLdsOctavePx / 4 + (size_t)kMaxLevels * kLdsTapStride) *
+    sizeof(double);
 // planes live in LDS with an odd row stride (W | 1 doubles: lane-per-row
 // accesses spread over the banks); an octave fits when its level and the
 // next octave's base do
