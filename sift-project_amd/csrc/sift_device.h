@@ -61,6 +61,22 @@ __device__ __forceinline__ double pow2i(int e) { return ldexp(1.0, e); }
 // vmcnt and lgkmcnt). Viewing them in address space 1 gives global loads.
 typedef __attribute__((address_space(1))) const double gdouble;
 __device__ __forceinline__ gdouble* gbl(const double* p) { return (gdouble*)p; }
+// ... and for stores (a generic-pointer store is a FLAT store, counted in
+// lgkmcnt too: every later LDS wait of the wave would also wait for it)
+typedef __attribute__((address_space(1))) double gdouble_w;
+__device__ __forceinline__ gdouble_w* gbl_w(double* p) { return (gdouble_w*)p; }
+
+// lane l's value of a per-lane table (wave-uniform result, no memory access)
+__device__ __forceinline__ int readlane_i32(int v, int l) {
+    return __builtin_amdgcn_readlane(v, l);
+}
+template <class T>
+__device__ __forceinline__ T* readlane_ptr(T* p, int l) {
+    const unsigned long long u = reinterpret_cast<unsigned long long>(p);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
 
 // Plane of level l of octave o of image b of the job (one pyramid arena per
 // image, identical layouts img_stride doubles apart).

@@ -516,12 +516,14 @@ struct LdsLevel {
 
 // A level's output pixel: the plane in LDS and in global memory, and the
 // next octave's base (resize_inter_nearest, image.cpp:41-55) when due.
+// (global-address-space stores: generic ones are FLAT stores, which count in
+// lgkmcnt as well, so later LDS waits of the wave would also wait for them)
 __device__ __forceinline__ void lds_put(const LdsLevel& L, int x, int y, double o) {
     L.A[y * L.P + x] = o;
-    L.g[y * L.W + x] = o;
+    gbl_w(L.g)[y * L.W + x] = o;
     if (L.dec && !(x & 1) && !(y & 1) && (x >> 1) < L.Wd && (y >> 1) < L.Hd) {
         L.D[(y >> 1) * L.Pd + (x >> 1)] = o;
-        L.gd[(y >> 1) * L.Wd + (x >> 1)] = o;
+        gbl_w(L.gd)[(y >> 1) * L.Wd + (x >> 1)] = o;
     }
 }
 
@@ -598,10 +600,17 @@ __device__ void lds_level(const LdsLevel& L, const double* __restrict__ tp) {
     __syncthreads();
 }
 
+// diagnostics hook of the LDS-octave kernel: called at phase boundaries (a
+// no-op here; tools/lds_lab.hip stamps s_memtime there)
+struct LdsNoHook {
+    __device__ void operator()() const {}
+};
+
 // Levels of at most kLdsTinyPx pixels (1080p: 30x16 and below): one output
 // per thread, a pass is a single short task per thread
-template <int R>
-__device__ void lds_level_tiny(const LdsLevel& L, const double* __restrict__ tp) {
+template <int R, class Hook = LdsNoHook>
+__device__ void lds_level_tiny(const LdsLevel& L, const double* __restrict__ tp,
+                               Hook sub = Hook{}) {
     double k[R + 1];
 #pragma unroll
     for (int u = 0; u <= R; ++u) k[u] = tp[u];
@@ -615,7 +624,9 @@ __device__ void lds_level_tiny(const LdsLevel& L, const double* __restrict__ tp)
         for (int u = 1; u <= R; ++u) acc += k[u] * (row[min(x + u, W - 1)] + row[max(x - u, 0)]);
         L.T[y * P + x] = div_sum_w(acc, sw, inv);
     }
+    sub();
     __syncthreads();
+    sub();
     for (int i = threadIdx.x; i < W * H; i += blockDim.x) {
         const int y = i / W, x = i - y * W;
         double acc = L.T[y * P + x] * k[0];
@@ -624,6 +635,7 @@ __device__ void lds_level_tiny(const LdsLevel& L, const double* __restrict__ tp)
             acc += k[u] * (L.T[min(y + u, H - 1) * P + x] + L.T[max(y - u, 0) * P + x]);
         lds_put(L, x, y, div_sum_w(acc, sw, inv));
     }
+    sub();
     __syncthreads();
 }
 
@@ -652,14 +664,42 @@ __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
     __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
-                                                      int o_first, int o_last, int n_gauss,
-                                                      const BlurTaps* __restrict__ taps) {
-    set_job_prio(pt->jp, SIFT_PRIO_LDS);
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int tid = threadIdx.x, nt = blockDim.x;
+// per-lane tables of the launch (every wave holds them; v_readlane gives a
+// level's values with no memory access in the level loop)
+struct LdsTables {
+    // lane i + 64 j of pl<j>: plane (octave o_first + (i + 64 j) / n_gauss,
+    // level (i + 64 j) % n_gauss)
+    const double *pl0, *pl1, *pl2;
+    int w, h;  // lane i: dims of octave o_first + i
+    int r;     // lane l: radius of level l
+    __device__ const double* plane_of(int idx) const {
+        const int j = idx >> 6, i = idx & 63;
+        return readlane_ptr(j == 0 ? pl0 : (j == 1 ? pl1 : pl2), i);
+    }
+};
+
+// the kernel's body; `hook()` runs after the base load, every level and
+// every octave, `sub()` inside the tiny levels (no-ops here; tools/
+// lds_lab.hip stamps s_memtime there)
+template <class Hook, class Sub = LdsNoHook>
+__device__ __forceinline__ void octaves_lds_run(const PyrTable* __restrict__ pt, int o_first,
+                                                int o_last, int n_gauss,
+                                                const BlurTaps* __restrict__ taps, double* lds,
+                                                Hook hook, Sub sub = Sub{}) {
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
     const int dec_level = n_gauss - 3;
     const int b = blockIdx.x;                           // image of the job
+    const int n_oct = o_last - o_first + 1;             // <= kMaxOctaves
+    LdsTables tb;
+    auto entry = [&](int i) -> const double* {
+        return i < n_oct * n_gauss ? plane(pt, b, o_first + i / n_gauss, i % n_gauss) : nullptr;
+    };
+    tb.pl0 = entry(lane);
+    tb.pl1 = entry(lane + 64);
+    tb.pl2 = entry(lane + 128);
+    tb.w = lane < n_oct ? pt->w[o_first + lane] : 0;
+    tb.h = lane < n_oct ? pt->h[o_first + lane] : 0;
+    tb.r = lane < n_gauss ? taps[lane].R : 0;
     // the level's plane lives in the large region A, the next octave's base
     // in the quarter region D; the roles swap from octave to octave (the
     // next octave's levels fit in the quarter region), so no copy
@@ -676,52 +716,65 @@ __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict
         TP[i] = v;
     }
     {
-        const int W = pt->w[o_first], H = pt->h[o_first], P = W | 1;
-        const double* g0 = plane(pt, b, o_first, 0);
+        const int W = readlane_i32(tb.w, 0), H = readlane_i32(tb.h, 0), P = W | 1;
+        gdouble* g0 = gbl(tb.plane_of(0));
         for (int i = tid; i < W * H; i += nt) {
             const int y = i / W;
             A[y * P + (i - y * W)] = g0[i];
         }
     }
     __syncthreads();
+    hook();
     for (int o = o_first; o <= o_last; ++o) {
+        const int oi = o - o_first;
         const bool has_next = o < o_last;
         LdsLevel L;
         L.A = A;
         L.T = T;
         L.D = D;
-        L.W = pt->w[o];
-        L.H = pt->h[o];
+        L.W = readlane_i32(tb.w, oi);
+        L.H = readlane_i32(tb.h, oi);
         L.P = L.W | 1;
-        L.Wd = has_next ? pt->w[o + 1] : 0;
-        L.Hd = has_next ? pt->h[o + 1] : 0;
+        L.Wd = has_next ? readlane_i32(tb.w, oi + 1) : 0;
+        L.Hd = has_next ? readlane_i32(tb.h, oi + 1) : 0;
         L.Pd = L.Wd | 1;
-        L.gd = has_next ? const_cast<double*>(plane(pt, b, o + 1, 0)) : nullptr;
+        L.gd = has_next ? const_cast<double*>(tb.plane_of((oi + 1) * n_gauss)) : nullptr;
         const bool tiny = L.W * L.H <= kLdsTinyPx;
         for (int l = 1; l < n_gauss; ++l) {
-            L.g = const_cast<double*>(plane(pt, b, o, l));
+            L.g = const_cast<double*>(tb.plane_of(oi * n_gauss + l));
             L.dec = has_next && l == dec_level;
             const double* tp = TP + l * kLdsTapStride;
-            switch (taps[l].R) {
+            switch (readlane_i32(tb.r, l)) {
 #define SIFT_LDS_CASE(RR)                                      \
     case RR:                                                   \
-        if (tiny) lds_level_tiny<RR>(L, tp);                   \
+        if (tiny) lds_level_tiny<RR>(L, tp, sub);              \
         else lds_level<RR>(L, tp);                             \
         break;
                 SIFT_LDS_CASE(1) SIFT_LDS_CASE(2) SIFT_LDS_CASE(3) SIFT_LDS_CASE(4)
                 SIFT_LDS_CASE(5) SIFT_LDS_CASE(6) SIFT_LDS_CASE(7) SIFT_LDS_CASE(8)
                 SIFT_LDS_CASE(9) SIFT_LDS_CASE(10) SIFT_LDS_CASE(11) SIFT_LDS_CASE(12)
-                SIFT_LDS_CASE(13) SIFT_LDS_CASE(14) SIFT_LDS_CASE(15) SIFT_LDS_CASE(16)
 #undef SIFT_LDS_CASE
-                default:
+                default:  // R > 12 (intervals <= 2, larger sigmas): templated
+                          // radii beyond 12 would push the 1024-thread kernel
+                          // past 128 VGPRs into scratch
                     lds_level_any(L, taps[l]);
             }
+            hook();
         }
         // the next octave's base (row stride Pd) becomes the current level
         double* t = A;
         A = D;
         D = t;
+        hook();
     }
+}
+
+__global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
+                                                      int o_first, int o_last, int n_gauss,
+                                                      const BlurTaps* __restrict__ taps) {
+    set_job_prio(pt->jp, SIFT_PRIO_LDS);
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, LdsNoHook{});
 }
 
 // Generic fallbacks for kernels wider than kMaxTemplR (unusual sigmas): a

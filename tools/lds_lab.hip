@@ -1,10 +1,9 @@
 // lds_lab.hip — where k_octaves_lds (the small octaves, one workgroup) spends
-// its time: the library kernel timed with events, and a stamped copy of its
-// octave / level loop (same device functions: lds_level<R>, lds_level_any)
-// that records s_memtime after each phase. Octaves as a W0 x H0 image's
+// its time: the library kernel timed with events, and its body (octaves_lds_run)
+// instantiated with a hook that records s_memtime after each phase. Octaves as a W0 x H0 image's
 // pyramid from octave o_first on (intervals 3, sigma 1.6).
 //
-//   lds_lab W0 H0 o_first o_last
+//   lds_lab W0 H0 o_first o_last [same_level]
 //
 // Test tooling only: includes the library's kernel translation unit.
 #include "../sift-project_amd/csrc/sift_kernels.hip"
@@ -30,80 +29,37 @@ namespace {
 
 constexpr int kMaxStamps = 256;
 
-// k_octaves_lds's loop with a stamp after the taps + base load, every level
-// and every octave (thread 0, vector store of a VGPR copy)
+// k_octaves_lds's body (octaves_lds_run) with a stamp after the taps + base
+// load, every level and every octave (thread 0, vector store of a VGPR copy)
+struct Stamp {
+    unsigned long long* stamps;
+    int* ns;
+    __device__ void operator()() const {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (threadIdx.x == 0) {
+            volatile unsigned long long* p = stamps + *ns;
+            *p = t;
+        }
+        ++*ns;
+    }
+};
+
 __global__ __launch_bounds__(1024) void k_octaves_lds_stamped(const PyrTable* __restrict__ pt,
                                                               int o_first, int o_last,
                                                               int n_gauss,
                                                               const BlurTaps* __restrict__ taps,
-                                                              unsigned long long* stamps) {
+                                                              unsigned long long* stamps,
+                                                              unsigned long long* sub_stamps) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int tid = threadIdx.x, nt = blockDim.x;
-    const int dec_level = n_gauss - 3;
     int ns = 0;
-    auto stamp = [&]() {
-        const unsigned long long t = __builtin_amdgcn_s_memtime();
-        if (tid == 0) {
-            volatile unsigned long long* p = stamps + ns;
-            *p = t;
-        }
-        ++ns;
-    };
-    stamp();
-    double* A = lds;
-    double* T = lds + kLdsOctavePx;
-    double* D = lds + 2 * kLdsOctavePx;
-    double* const TP = lds + 2 * kLdsOctavePx + kLdsOctavePx / 4;
-    for (int i = tid; i < n_gauss * kLdsTapStride; i += nt) {
-        const int l = i / kLdsTapStride, j = i - l * kLdsTapStride;
-        const BlurTaps& t = taps[l];
-        double v = 0.0;
-        if (j <= kMaxTemplR) v = j <= t.R ? t.k[j] : 0.0;
-        else v = j == kMaxTemplR + 1 ? t.sum_w : t.inv;
-        TP[i] = v;
-    }
-    {
-        const int W = pt->w[o_first], H = pt->h[o_first], P = W | 1;
-        const double* g0 = plane(pt, 0, o_first, 0);
-        for (int i = tid; i < W * H; i += nt) {
-            const int y = i / W;
-            A[y * P + (i - y * W)] = g0[i];
-        }
-    }
-    __syncthreads();
-    stamp();
-    for (int o = o_first; o <= o_last; ++o) {
-        const bool has_next = o < o_last;
-        LdsLevel L;
-        L.A = A;
-        L.T = T;
-        L.D = D;
-        L.W = pt->w[o];
-        L.H = pt->h[o];
-        L.P = L.W | 1;
-        L.Wd = has_next ? pt->w[o + 1] : 0;
-        L.Hd = has_next ? pt->h[o + 1] : 0;
-        L.Pd = L.Wd | 1;
-        L.gd = has_next ? const_cast<double*>(plane(pt, 0, o + 1, 0)) : nullptr;
-        const bool tiny = L.W * L.H <= kLdsTinyPx;
-        for (int l = 1; l < n_gauss; ++l) {
-            L.g = const_cast<double*>(plane(pt, 0, o, l));
-            L.dec = has_next && l == dec_level;
-            const double* tp = TP + l * kLdsTapStride;
-            switch (taps[l].R) {
-                case 4: tiny ? lds_level_tiny<4>(L, tp) : lds_level<4>(L, tp); break;
-                case 5: tiny ? lds_level_tiny<5>(L, tp) : lds_level<5>(L, tp); break;
-                case 6: tiny ? lds_level_tiny<6>(L, tp) : lds_level<6>(L, tp); break;
-                case 8: tiny ? lds_level_tiny<8>(L, tp) : lds_level<8>(L, tp); break;
-                case 10: tiny ? lds_level_tiny<10>(L, tp) : lds_level<10>(L, tp); break;
-                default: lds_level_any(L, taps[l]);
-            }
-            stamp();
-        }
-        double* t = A;
-        A = D;
-        D = t;
-        stamp();
+    const Stamp st{stamps, &ns};
+    st();
+    if (sub_stamps) {
+        int ns2 = 0;
+        const Stamp sub{sub_stamps, &ns2};
+        octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, st, sub);
+    } else {
+        octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, st);
     }
 }
 
@@ -116,6 +72,9 @@ int main(int argc, char** argv) {
     }
     const int W0 = std::atoi(argv[1]), H0 = std::atoi(argv[2]);
     const int o_first = std::atoi(argv[3]), o_last = std::atoi(argv[4]);
+    // optional: every level with the sigma of level `same` (same code path
+    // for all levels: separates per-level instruction fetch from the work)
+    const int same = argc > 5 ? std::atoi(argv[5]) : 0;
     const int n_gauss = 6;
     PyrTable h{};
     std::vector<double*> bufs;
@@ -139,7 +98,7 @@ int main(int argc, char** argv) {
     std::vector<BlurTaps> taps(n_gauss);
     const double s0 = 1.6, k = std::pow(2.0, 1.0 / 3.0);
     for (int l = 1; l < n_gauss; ++l) {
-        const double sg = std::pow(k, l - 1) * s0 * std::sqrt(k * k - 1);
+        const double sg = std::pow(k, (same ? same : l) - 1) * s0 * std::sqrt(k * k - 1);
         BlurTaps& t = taps[l];
         t.R = (int)std::ceil(3 * sg);
         double sw = 0;
@@ -156,6 +115,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_pt, sizeof h));
     CK(hipMalloc(&d_taps, taps.size() * sizeof(BlurTaps)));
     CK(hipMalloc(&d_st, kMaxStamps * 8));
+    unsigned long long* d_sub;
+    CK(hipMalloc(&d_sub, kMaxStamps * 8));
     CK(hipMemcpy(d_pt, &h, sizeof h, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_taps, taps.data(), taps.size() * sizeof(BlurTaps), hipMemcpyHostToDevice));
     CK(prepare_kernel_attributes());
@@ -181,7 +142,7 @@ int main(int argc, char** argv) {
     int n = 0;
     for (int r = 0; r < reps; ++r) {
         hipLaunchKernelGGL(k_octaves_lds_stamped, dim3(1), dim3(1024), kLdsOctaveBytes, 0, d_pt,
-                           o_first, o_last, n_gauss, d_taps, d_st);
+                           o_first, o_last, n_gauss, d_taps, d_st, nullptr);
         CK(hipGetLastError());
         CK(hipDeviceSynchronize());
         std::vector<unsigned long long> st(kMaxStamps);
@@ -200,6 +161,39 @@ int main(int argc, char** argv) {
         }
         std::printf("  octave end %4.0f  sum %7.0f\n", acc[i], tot + acc[i]);
         ++i;
+    }
+    // phases inside the tiny levels: row pass, barrier, column pass, barrier
+    std::vector<double> ph(4 * kMaxStamps, 0.0);
+    for (int r = 0; r < reps; ++r) {
+        hipLaunchKernelGGL(k_octaves_lds_stamped, dim3(1), dim3(1024), kLdsOctaveBytes, 0, d_pt,
+                           o_first, o_last, n_gauss, d_taps, d_st, d_sub);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        std::vector<unsigned long long> st(kMaxStamps), su(kMaxStamps);
+        CK(hipMemcpy(st.data(), d_st, kMaxStamps * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(su.data(), d_sub, kMaxStamps * 8, hipMemcpyDeviceToHost));
+        int q = 0;
+        for (int o = o_first; o <= o_last; ++o) {
+            if (h.w[o] * h.h[o] > kLdsTinyPx) continue;
+            for (int l = 1; l < n_gauss; ++l, ++q) {
+                const int e = 2 + (o - o_first) * n_gauss + (l - 1);
+                const double t0 = (double)st[e - 1], t3 = (double)st[e];
+                const double a = (double)su[3 * q], b = (double)su[3 * q + 1],
+                             c = (double)su[3 * q + 2];
+                ph[4 * q] += (a - t0) / reps;
+                ph[4 * q + 1] += (b - a) / reps;
+                ph[4 * q + 2] += (c - b) / reps;
+                ph[4 * q + 3] += (t3 - c) / reps;
+            }
+        }
+    }
+    std::printf("tiny levels (cycles): row pass | barrier | column pass | barrier\n");
+    int q = 0;
+    for (int o = o_first; o <= o_last; ++o) {
+        if (h.w[o] * h.h[o] > kLdsTinyPx) continue;
+        for (int l = 1; l < n_gauss; ++l, ++q)
+            std::printf("  octave %2d L%d (R%2d): %6.0f %6.0f %6.0f %6.0f\n", o, l, taps[l].R,
+                        ph[4 * q], ph[4 * q + 1], ph[4 * q + 2], ph[4 * q + 3]);
     }
     for (double* p : bufs) (void)hipFree(p);
     return 0;
