@@ -259,8 +259,7 @@ struct sift_ctx {
     // 384 came back ahead: -2.3 % over 6 interleaved runs of the driver's
     // command (profiles/r04_ab r04_ee; 512 descriptor workgroups +0.7 %,
     // 96 orientation +1.5 %). Jobs alone: x1.5, or the whole chip for a
-    // launch with nothing beside it (enqueue_chain). SIFT_KP_WGS /
-    // SIFT_DESC_WGS (tuning).
+    // launch with nothing beside it (enqueue_chain).
     unsigned kp_wgs = 192;
     unsigned desc_wgs = 384;  // k_descriptor_split: ONE record per workgroup
     // octaves of >= 2^this pixels (x images) get their own keypoint batch; the
@@ -309,9 +308,9 @@ struct sift_ctx {
     // bursts). Launch graphs per slot cut the host's enqueue from 0.12 to
     // 0.03 ms per job but ran the step 2 % slower (profiles/r03_j): removed.
     int pipe_hint = 0;
-    long ext_waves = 512;   // SIFT_EXT_WAVES: extrema tasks per octave (extrema_grid)
-    int ext_seg_max = 32;   // SIFT_EXT_SEGMAX: centre rows per extrema task, at most
-    // Pyramid token (SIFT_PYR_CHAIN): a job's pyramid waits for the previous
+    long ext_waves = 512;   // extrema tasks per octave (extrema_grid)
+    int ext_seg_max = 32;   // centre rows per extrema task, at most
+    // Pyramid token: a job's pyramid waits for the previous
     // job's octave 0 (an event). In the steady state of a pipeline it is long
     // built; a burst of jobs submitted together (a pipeline filling) would
     // otherwise run their HBM-bound octave-0 blurs side by side and then
@@ -1267,8 +1266,6 @@ int sift_hip_create(int device, sift_ctx** out) {
     ctx->device = device;
     int prio_lo = 0, prio_hi = 0;  // numerically lower = higher priority
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
-    if (const char* e = std::getenv("SIFT_KP_WGS")) ctx->kp_wgs = (unsigned)std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_DESC_WGS")) ctx->desc_wgs = (unsigned)std::max(1, std::atoi(e));
     if (const char* e = std::getenv("SIFT_BATCH_PX_LOG2")) {
         const int v = std::atoi(e);
         if (v >= 0 && v <= 40) ctx->batch_px_log2 = ctx->batch_px_log2_alone = v;
@@ -1276,11 +1273,6 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_LDS_PX"))
         ctx->lds_max_px = ctx->lds_max_px_shared = (size_t)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_LDS_PX_SHARED"))
-        ctx->lds_max_px_shared = (size_t)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_EXT_WAVES")) ctx->ext_waves = std::max(64L, std::atol(e));
-    if (const char* e = std::getenv("SIFT_EXT_SEGMAX")) ctx->ext_seg_max = std::max(4, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_PYR_CHAIN")) ctx->pyr_chain = std::atoi(e) != 0;
     bool ok = prepare_kernel_attributes() == hipSuccess;
     ok = ok && hipMalloc(&ctx->d_done, sizeof(unsigned)) == hipSuccess &&
          hipMemset(ctx->d_done, 0, sizeof(unsigned)) == hipSuccess;
