@@ -795,43 +795,37 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         }
         return run_chain(L, o_begin, o_end, gb < lanes ? zeros : snap(gb - lanes), snap(gb));
     };
-    // The pyramid alternates between two streams, octave o on pyr[o % 2]:
-    // octave o+1 only needs the decimated level `intervals` of octave o, so it
-    // starts as soon as that level exists and overlaps the last two levels of
-    // octave o (the small octaves are latency-bound: two in flight at once).
-    hipStream_t pyr[2] = {sA, sB};
-    hipEvent_t base_ready = nullptr;  // next octave's base written (decimation)
-    // cross-stream events only where the two pyramid streams differ (a job
-    // on one stream is ordered by the stream itself: fewer API calls)
+    // Two pyramid streams (a job alone): the decimation chain on A — levels
+    // 1 .. intervals of every octave, octave o+1 needs only level
+    // `intervals` of octave o (sift.cpp:195-196) — and each octave's two
+    // tail levels on B after an event on A, so the chain never queues behind
+    // a tail (round 4 alternated whole octaves between A and B: octave 2
+    // waited on A behind octave 0's R = 8 / 10 levels, ~80 us on 1080p,
+    // and every octave switch paid a cross-stream join on the chain).
+    // One stream (a pipelined job): in order.
     const bool two_pyr = sA != sB;
-    if (two_pyr && (o_small > 0 || o_small < g.octaves)) {
-        // stream B's first octave must also see the input staging on A
-        base_ready = sync_event(s);
-        if (!base_ready) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(base_ready, sA));
-    }
     for (int o = 0; o < o_small; ++o) {
-        hipStream_t so = pyr[o & 1];
-        if (o > 0 && two_pyr) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
         for (int l = 1; l < g.n_gauss; ++l) {
+            const bool tail = two_pyr && l > dec_level;
+            hipStream_t so = tail ? sB : sA;
+            if (tail && l == dec_level + 1) {
+                hipEvent_t chain_ev = sync_event(s);
+                if (!chain_ev) return SIFT_ERR_HIP;
+                SIFT_HIP_TRY(hipEventRecord(chain_ev, sA));
+                SIFT_HIP_TRY(hipStreamWaitEvent(sB, chain_ev, 0));
+            }
             const bool dec = (l == dec_level) && (o + 1 < g.octaves);
             if ((st = blur(so, o, l, s.h_pt.lvl[o][l - 1], stride, s.taps[l], dec)) != SIFT_OK)
                 return st;
-            if (dec && two_pyr) {
-                base_ready = sync_event(s);
-                if (!base_ready) return SIFT_ERR_HIP;
-                SIFT_HIP_TRY(hipEventRecord(base_ready, so));
-            }
         }
         if (o == 0 && ctx->pyr_chain) {
-            SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, so));
+            SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, two_pyr ? sB : sA));
             ctx->pyr_last = (int)(&s - ctx->slots);
         }
-        if (o < o_merge && (st = batch(o, o + 1, {so})) != SIFT_OK) return st;
+        if (o < o_merge && (st = batch(o, o + 1, {sA, sB})) != SIFT_OK) return st;
     }
-    if (o_small < g.octaves) {
-        hipStream_t so = pyr[o_small & 1];
-        if (two_pyr) SIFT_HIP_TRY(hipStreamWaitEvent(so, base_ready, 0));
+    if (o_small < g.octaves) {  // on the chain stream, after the last decimation
+        hipStream_t so = sA;
         double bytes = 0.0;
         for (int o = o_small; o < g.octaves; ++o) {
             bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[o] * (double)g.H[o];

@@ -1215,6 +1215,16 @@ __global__ __launch_bounds__(NT) void k_refine(const PyrTable* __restrict__ pt, 
 // pori), and the kept one is described from its own fields. (One fused
 // orientation+descriptor kernel was measured slower: 242 VGPRs, 2 waves/SIMD.)
 // ---------------------------------------------------------------------------
+// lane i <- lane i-1 (DPP wavefront shift right); lane 0 <- fill
+__device__ __forceinline__ double wave_shr1_f64(double v, double fill) {
+    const unsigned long long u = __double_as_longlong(v), f = __double_as_longlong(fill);
+    const unsigned lo =
+        __builtin_amdgcn_update_dpp((unsigned)f, (unsigned)u, 0x138, 0xf, 0xf, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp((unsigned)(f >> 32), (unsigned)(u >> 32),
+                                                    0x138, 0xf, 0xf, false);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const unsigned long long u = __double_as_longlong(v);
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
@@ -1449,20 +1459,27 @@ __global__ __launch_bounds__(256, 4) void k_orient_wave(
 #pragma unroll
                 for (int q = 0; q < kOriWReps; ++q)
                     h += hist[lane * kOriWReps + ((q + lane) & (kOriWReps - 1))];
+            // The recurrence runs across the lanes: every step, lane i
+            // re-evaluates fma(0.25, h_new[i-1], c_i) + d_i from lane i-1's
+            // current value (DPP wavefront shift; lane 0 takes the old
+            // h[nb-1]), so lane i is final from step i on: nb steps of 4
+            // VALU instructions instead of ~10 (readlanes and a select per
+            // bin); the same operands in the same order, bit-identical.
             for (int it = 0; it < kSmoothIters; ++it) {
                 const double hn = __shfl(h, lane + 1 < nb ? lane + 1 : 0);  // old h[i+1]
-                const double c = 0.5 * h, d = 0.25 * hn;
-                double prev = readlane_f64(h, nb - 1);  // h[i-1] for i = 0: old
-                double first_new = 0.0, mine = h;
+                const double c = 0.5 * h;
+                double d = 0.25 * hn;
+                const double hlast = readlane_f64(h, nb - 1);  // h[i-1] for i = 0: old
+                double v = h;
                 for (int i = 0; i < nb; ++i) {
-                    const double ci = readlane_f64(c, i);
-                    const double dn = (i + 1 == nb && i > 0) ? 0.25 * first_new : readlane_f64(d, i);
-                    const double v = fma(0.25, prev, ci) + dn;
-                    if (lane == i) mine = v;
-                    prev = v;
-                    if (i == 0) first_new = v;
+                    v = fma(0.25, wave_shr1_f64(v, hlast), c) + d;
+                    if (i == 0 && nb > 1) {
+                        // in place: the last bin's h[i+1] is the new h[0]
+                        const double first_new = readlane_f64(v, 0);
+                        if (lane == nb - 1) d = 0.25 * first_new;
+                    }
                 }
-                h = mine;
+                h = v;
             }
             double mx = lane < nb ? h : 0.0;  // bins >= 0
 #pragma unroll
