@@ -193,6 +193,10 @@ struct Slot {
     unsigned* h_ctr = nullptr;  // pinned, live counters of every lane
     Stage* h_stage = nullptr;
     Stage* d_stage = nullptr;
+    // what d_stage holds, age ranks zeroed (valid once uploaded): a job with
+    // the same tables only sets its rank (k_job_begin)
+    Stage stage_dev{};
+    bool stage_valid = false;
     PyrTable h_pt{};
     Pinned<uint8_t> h_up;  // pinned upload staging
     // records exported by k_descriptor per keypoint chain (mapped pinned)
@@ -637,11 +641,26 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     s.h_pt.n_img = n_img;
     s.h_pt.n_oct = g.octaves;
     s.h_pt.jp = s.taps_init.jp;
-    // the slot's previous job has been fetched, so its copy out of h_stage
-    // has completed and the staging can be rewritten
-    s.h_stage->pt = s.h_pt;
-    for (int l = 0; l < g.n_gauss; ++l) s.h_stage->taps[l] = s.taps[l];
-    SIFT_HIP_TRY(hipMemcpyAsync(s.d_stage, s.h_stage, sizeof(Stage), hipMemcpyHostToDevice, sA));
+    // the tables' device copy is uploaded only when they change (geometry,
+    // parameters, buffers); the age rank is set by k_job_begin below. The
+    // slot's previous job has been fetched, so its copy out of h_stage has
+    // completed and the staging can be rewritten.
+    {
+        Stage cur;
+        std::memset(&cur, 0, sizeof cur);  // padding included: compared bytewise
+        cur.pt = s.h_pt;
+        for (int l = 0; l < g.n_gauss; ++l) cur.taps[l] = s.taps[l];
+        cur.pt.jp = JobPrio{};
+        for (int l = 0; l < g.n_gauss; ++l) cur.taps[l].jp = JobPrio{};
+        if (!s.stage_valid || std::memcmp(&cur, &s.stage_dev, sizeof cur) != 0) {
+            s.stage_valid = false;
+            std::memcpy(s.h_stage, &cur, sizeof cur);
+            SIFT_HIP_TRY(
+                hipMemcpyAsync(s.d_stage, s.h_stage, sizeof(Stage), hipMemcpyHostToDevice, sA));
+            s.stage_dev = cur;
+            s.stage_valid = true;
+        }
+    }
     const PyrTable* d_pt = &s.d_stage->pt;
 
     // wide kernels (R > kMaxTemplR) go through a temporary: one per pyramid
@@ -661,7 +680,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
 
     const int lanes = s.lanes;
     hipStream_t lane_stream[kLanes] = {sC, sD};
-    SIFT_HIP_TRY(hipMemsetAsync(s.d_ctr, 0, kCtrWords * sizeof(unsigned), sA));
+    SIFT_HIP_TRY(launch_job_begin(&s.d_stage->pt, s.h_pt.jp, s.d_ctr, kCtrWords, sA));
 
     auto blur = [&](hipStream_t so, int o, int l, const double* bsrc, size_t src_bs,
                     const BlurTaps& t, bool dec) -> int {

@@ -20,12 +20,16 @@ hipError_t prepare_kernel_attributes();
 // Batched launches: n_img images of one job, image b's planes `bs` doubles
 // after image 0's (src, dst and dec alike), blockIdx.z = image.
 hipError_t launch_u8_to_f64(const uint8_t* in, double* out, size_t n, hipStream_t s);
+// zero a job's counters and set its age rank in its device tables
+hipError_t launch_job_begin(PyrTable* pt, const JobPrio& jp, unsigned* ctr, int n_ctr,
+                            hipStream_t s);
 hipError_t launch_prepare(const double* in, size_t in_bs, int w, int h, int c, int dbl,
                           double* out, size_t out_bs, int W0, int H0, int n_img, hipStream_t s);
 // e0/e1: optional HIP events timestamped by the dispatch itself (profiling);
 // tmp: n_img * W * H doubles for kernels wider than kMaxTemplR
 // planes of at most tile_max_px pixels use the LDS-tile kernel (k_blur_tile),
-// larger ones the strip walk (k_blur)
+// planes of >= 4 Mpx the pair walk (k_blur_pair), the others the strip walk
+// (k_blur)
 hipError_t launch_blur(const double* src, size_t src_bs, double* dst, size_t bs, int n_img, int W,
                        int H, const BlurTaps& taps, double* dec, int Wd, int Hd, double* tmp,
                        hipStream_t s, hipEvent_t e0, hipEvent_t e1, size_t tile_max_px);

@@ -50,6 +50,21 @@
 #ifndef SIFT_BLUR_BIG_COLS
 #define SIFT_BLUR_BIG_COLS 2
 #endif
+// Gaussian planes >= 4 Mpx: k_blur_pair (1) or the strip walk k_blur (0).
+// Pair walk, 2 columns per lane, 32 rows per wave, against the strip walk
+// (tools/blur_lab.hip, r05_lab6; every output bit-identical): 3840x2160
+// levels R = 4..10 169.0 vs 174.8 us, 8192^2 R = 5..14 1086 vs 1207 us,
+// 15360x8640 2349 vs 2507 us (the R = 10 levels -10..-12 %); one column per
+// lane 171.0 / 1288 / 2688 us; driver's bench 0.557 vs 0.565 ms per step.
+#ifndef SIFT_BLUR_PAIR
+#define SIFT_BLUR_PAIR 1
+#endif
+#ifndef SIFT_BLUR_PAIR_COLS  // k_blur_pair: columns per lane (1 or 2)
+#define SIFT_BLUR_PAIR_COLS 2
+#endif
+#ifndef SIFT_BLUR_PAIR_ROWS  // k_blur_pair: output rows per wave (a pair: twice that)
+#define SIFT_BLUR_PAIR_ROWS 32
+#endif
 #ifndef SIFT_ORI_AHEAD  // k_orient_wave: steps of 64 samples whose loads are in flight
 #define SIFT_ORI_AHEAD 1
 #endif
@@ -365,6 +380,172 @@ __global__ __launch_bounds__(256) void k_blur(BlurSource src, double* __restrict
 #undef SIFT_UP_HX
 
 // ---------------------------------------------------------------------------
+// k_blur_pair<R, C, DECIM>: the same level (image.cpp:156-214) for Gaussian
+// planes of octave-0 size, walked by PAIRS of wavefronts. A workgroup's four
+// waves are two pairs; a pair owns 2*rows output rows of a strip of 64*C
+// columns, split at its boundary row b: the down wave produces rows
+// [b, b+rows) walking down, the up wave rows [b-rows, b) walking up. Each
+// wave first evaluates the row pass of the R source rows on its side of b —
+// the first R rows of its own column window and the first R rows of its
+// partner's — and hands them over through LDS (one workgroup barrier). A
+// wave thus evaluates R + rows row passes for `rows` outputs where the strip
+// walk of k_blur evaluates 2R + rows: at R = 10 and 32 rows, 42 instead of
+// 52 (the walk's priming of 2R rows, halved).
+//
+// Walk position p of a wave is source row b - R + p (down) or b - 1 + R - p
+// (up); positions [R, 2R) are its own prologue rows, [0, R) its partner's
+// (partner position R + j = own position R - 1 - j), position 2R + k is
+// staged at walk step k, and step k >= 1 produces the output at position
+// R + k - 1 from window positions k - 1 .. k - 1 + 2R while the row pass of
+// position 2R + k is in flight (the two dependency chains overlap as in
+// k_blur). The PF rows in flight run on from the prologue into the walk.
+// The column pass sums the pairs k[u] * (v[+u] + v[-u]), whose IEEE
+// addition commutes, so the up wave's outputs are bit-identical to a
+// downward walk's; borders replicate by clamping the source row.
+// ---------------------------------------------------------------------------
+template <int R, int C, bool DECIM>
+__global__ __launch_bounds__(256) void k_blur_pair(const double* __restrict__ src, size_t src_bs,
+                                                   double* __restrict__ dst, size_t bs, int W,
+                                                   int H, int rows, BlurTaps taps,
+                                                   double* __restrict__ dec, int Wd, int Hd) {
+    set_job_prio(taps.jp, SIFT_PRIO_STRIP);
+    constexpr int PF = SIFT_BLUR_PF;
+    constexpr int NW = 2 * R + 2;
+    constexpr int SPAN = 64 * C;
+    constexpr int NL = (SPAN + 2 * R + 63) / 64;
+    __shared__ __attribute__((aligned(16))) double sline[4][64 * NL + 2];
+    __shared__ __attribute__((aligned(16))) double xch[4][R][SPAN];
+    static_assert(sizeof(sline) + sizeof(xch) <= 64 * 1024, "k_blur_pair: static LDS");
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool down = (wv & 1) != 0;
+    int bx, by, bz;
+    xcd_remap(bx, by, bz);
+    if (by * 4 * rows >= H) return;  // the whole workgroup lies below the image
+    src += bz * src_bs;
+    dst += bz * bs;
+    if (DECIM) dec += bz * bs;
+    const int x0 = bx * SPAN;
+    const int b = (2 * (by * 2 + (wv >> 1)) + 1) * rows;  // the pair's boundary row
+    double* const sl = sline[wv];
+    int gx[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) gx[q] = clampi(x0 - R + lane + 64 * q, 0, W - 1);
+    double k[R + 1];
+#pragma unroll
+    for (int u = 0; u <= R; ++u) k[u] = taps.k[u];
+    const double sw = taps.sum_w, inv = taps.inv;
+    // source row of walk position p (clamped: replicate border)
+    auto row_at = [&](int p) {
+        return clampi(down ? b - R + p : b - 1 + R - p, 0, H - 1);
+    };
+    double pf[PF][NL];
+    auto stage = [&](int p_next) {  // stage pf[0] in the LDS line, fetch position p_next
+#pragma unroll
+        for (int q = 0; q < NL; ++q) sl[lane + 64 * q] = pf[0][q];
+#pragma unroll
+        for (int p = 0; p + 1 < PF; ++p)
+#pragma unroll
+            for (int q = 0; q < NL; ++q) pf[p][q] = pf[p + 1][q];
+        const int ry = row_at(p_next);
+#pragma unroll
+        for (int q = 0; q < NL; ++q) pf[PF - 1][q] = src[(size_t)ry * W + gx[q]];
+    };
+    auto row_pass = [&](double* hn) {  // of the row staged in the LDS line
+        double v[C + 2 * R];
+        if (C == 2) {
+            const double2* s2 = reinterpret_cast<const double2*>(sl + 2 * lane);
+#pragma unroll
+            for (int q = 0; q < (C + 2 * R) / 2; ++q) {
+                const double2 t = s2[q];
+                v[2 * q] = t.x;
+                v[2 * q + 1] = t.y;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < C + 2 * R; ++q) v[q] = sl[lane + q];
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            double acc = v[c + R] * k[0];
+#pragma unroll
+            for (int u = 1; u <= R; ++u) acc += k[u] * (v[c + R + u] + v[c + R - u]);
+            hn[c] = div_sum_w(acc, sw, inv);
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+        const int ry = row_at(R + p);
+#pragma unroll
+        for (int q = 0; q < NL; ++q) pf[p][q] = src[(size_t)ry * W + gx[q]];
+    }
+    double win[C][NW];
+    // prologue: own positions R .. 2R-1 (their rows' horizontal pass), also
+    // handed to the partner
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        stage(R + j + PF);
+        wave_sync();
+        double hn[C];
+        row_pass(hn);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            win[c][R + j] = hn[c];
+            xch[wv][j][C * lane + c] = hn[c];
+        }
+        wave_sync();
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int c = 0; c < C; ++c) win[c][R - 1 - j] = xch[wv ^ 1][j][C * lane + c];
+    if (down ? b >= H : b - rows >= H) return;  // no output row of this wave in the image
+    const int xa = x0 + C * lane;
+    for (int kb = 0; kb <= rows; kb += NW) {
+#pragma unroll
+        for (int t = 0; t < NW; ++t) {
+            const int kk = kb + t;
+            if (kk <= rows) {
+                // (the last step's row pass is not needed; evaluating it keeps
+                // the row pass unconditional, so the compiler interleaves it
+                // with the column pass: skipping it cost ~10 %)
+                double hn[C];
+                stage(2 * R + kk + PF);
+                wave_sync();
+                row_pass(hn);
+                if (kk >= 1) {
+                    const int y = down ? b + kk - 1 : b - kk;
+                    double o[C];
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        double a = win[c][(t + R - 1 + NW) % NW] * k[0];
+#pragma unroll
+                        for (int u = 1; u <= R; ++u)
+                            a += k[u] * (win[c][(t + R - 1 + u) % NW] +
+                                         win[c][(t + R - 1 - u + 2 * NW) % NW]);
+                        o[c] = div_sum_w(a, sw, inv);
+                    }
+                    if (y < H && xa < W) {
+                        if (C == 2)  // W is even for C == 2 (launcher)
+                            *reinterpret_cast<double2*>(dst + (size_t)y * W + xa) =
+                                make_double2(o[0], o[C - 1]);
+                        else
+                            dst[(size_t)y * W + xa] = o[0];
+                        if (DECIM && !(y & 1) && (y >> 1) < Hd && (C == 2 || !(xa & 1)) &&
+                            (xa >> 1) < Wd)
+                            dec[(size_t)(y >> 1) * Wd + (xa >> 1)] = o[0];
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < C; ++c) win[c][(2 * R + t) % NW] = hn[c];
+                wave_sync();
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_blur_tile<R, DECIM>: the same level (image.cpp:156-214) for planes small
 // enough to be cache-resident (octaves >= 1 of a 1080p image), where the
 // strip walk of k_blur is latency-bound (2R+1+rows serial steps per wave).
@@ -534,7 +715,10 @@ __device__ __forceinline__ void lds_put(const LdsLevel& L, int x, int y, double 
 // and the odd stride P keeps those lanes on different banks. Runs of 4 (not
 // 8) put twice the waves on the level's FP64 work.
 constexpr int kLdsRun = 4;
-constexpr int kLdsTinyPx = 600;
+#ifndef SIFT_LDS_TINY_PX
+#define SIFT_LDS_TINY_PX 600
+#endif
+constexpr int kLdsTinyPx = SIFT_LDS_TINY_PX;
 
 template <int R>
 __device__ void lds_level(const LdsLevel& L, const double* __restrict__ tp) {
@@ -1571,6 +1755,32 @@ static hipError_t launch_blur_r(const BlurSource& src, double* dst, size_t bs, i
                         W, H, rows, taps, dec, Wd, Hd);
 }
 
+template <int R, int C>
+static hipError_t launch_pair_r(const double* src, size_t src_bs, double* dst, size_t bs,
+                                int n_img, int W, int H, int rows, const BlurTaps& taps,
+                                double* dec, int Wd, int Hd, hipStream_t s, hipEvent_t e0,
+                                hipEvent_t e1) {
+    const dim3 grid((W + 64 * C - 1) / (64 * C), (H + 4 * rows - 1) / (4 * rows), n_img);
+    if (dec)
+        return launch_timed(k_blur_pair<R, C, true>, grid, dim3(256), 0, s, e0, e1, src, src_bs,
+                            dst, bs, W, H, rows, taps, dec, Wd, Hd);
+    return launch_timed(k_blur_pair<R, C, false>, grid, dim3(256), 0, s, e0, e1, src, src_bs, dst,
+                        bs, W, H, rows, taps, dec, Wd, Hd);
+}
+using PairFn = hipError_t (*)(const double*, size_t, double*, size_t, int, int, int, int,
+                              const BlurTaps&, double*, int, int, hipStream_t, hipEvent_t,
+                              hipEvent_t);
+template <int C, int... Rs>
+struct PairTable {
+    static constexpr PairFn fns[sizeof...(Rs)] = {&launch_pair_r<Rs, C>...};
+};
+template <int C, int... Rs>
+constexpr PairFn PairTable<C, Rs...>::fns[sizeof...(Rs)];
+using BlurPair1 = PairTable<1, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
+// two columns per lane: the hand-over buffer (4 waves x R rows x 128
+// columns) fits the 64 KB of static LDS up to R = 14
+using BlurPair2 = PairTable<2, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14>;
+
 using BlurFn = hipError_t (*)(const BlurSource&, double*, size_t, int, int, int, int,
                               const BlurTaps&, double*, int, int, hipStream_t, hipEvent_t,
                               hipEvent_t);
@@ -1595,9 +1805,10 @@ using BlurUpsRGB2 = BlurTable<2, kSrcUpsampleRGB, SIFT_R_LIST>;
 static_assert(kMaxTemplR == 16, "blur tables must cover 1..kMaxTemplR");
 
 // Strip shape per level (measured on MI355X, tools/blur_lab.hip): two
-// columns per lane and 32-row strips on octave-0-sized levels, two columns
-// and 16 rows around 2 Mpx, one column and 16 rows below (more, shorter
-// strips: the small levels are latency-bound).
+// columns per lane and 32-row strips on octave-0-sized levels (the initial
+// blur fused with the input staging; the other octave-0 levels take
+// k_blur_pair), two columns and 16 rows around 2 Mpx, one column and 16 rows
+// below (more, shorter strips: the small levels are latency-bound).
 BlurShape blur_shape_for(int W, int H, int R) {
     const size_t px = (size_t)W * H;
     BlurShape b;
@@ -1657,6 +1868,12 @@ hipError_t launch_blur(const double* src, size_t src_bs, double* dst, size_t bs,
         return (dec ? TileDec::fns[R - 1] : TileNoDec::fns[R - 1])(src, src_bs, dst, bs, n_img, W,
                                                                    H, taps, dec, Wd, Hd, s, e0,
                                                                    e1);
+    if (R >= 1 && R <= kMaxTemplR && SIFT_BLUR_PAIR && (size_t)W * H >= ((size_t)4 << 20)) {
+        const int rows = std::min(SIFT_BLUR_PAIR_ROWS, (H + 1) / 2);
+        const bool two = SIFT_BLUR_PAIR_COLS == 2 && !(W & 1) && R <= 14;
+        return (two ? BlurPair2::fns : BlurPair1::fns)[R - 1](src, src_bs, dst, bs, n_img, W, H,
+                                                              rows, taps, dec, Wd, Hd, s, e0, e1);
+    }
     if (R >= 1 && R <= kMaxTemplR) {
         const BlurSource src_desc{src, src_bs, W, H, 1};
         return launch_blur_shaped(kSrcPlane, src_desc, dst, bs, n_img, W, H, taps, dec, Wd, Hd,
@@ -1725,6 +1942,22 @@ __global__ __launch_bounds__(256) void k_u8_to_f64(const uint8_t* __restrict__ i
     } else {
         for (size_t i = i0; i < n && i < i0 + 8; ++i) out[i] = (double)in[i];
     }
+}
+
+// A job's first device work besides its pyramid: zero its counters and set
+// its age rank in the (otherwise unchanged) device copy of its tables — one
+// small launch instead of a table upload (a copy kernel reading pinned host
+// memory, ~8 us) and a memset (~5 us) ahead of the first blur.
+__global__ __launch_bounds__(256) void k_job_begin(PyrTable* __restrict__ pt, JobPrio jp,
+                                                   unsigned* __restrict__ ctr, int n_ctr) {
+    for (int i = threadIdx.x; i < n_ctr; i += blockDim.x) ctr[i] = 0u;
+    if (threadIdx.x == 0) pt->jp = jp;
+}
+
+hipError_t launch_job_begin(PyrTable* pt, const JobPrio& jp, unsigned* ctr, int n_ctr,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_job_begin, dim3(1), dim3(256), 0, s, pt, jp, ctr, n_ctr);
+    return hipGetLastError();
 }
 
 hipError_t launch_u8_to_f64(const uint8_t* in, double* out, size_t n, hipStream_t s) {

@@ -77,19 +77,26 @@ def test_gpu_native_allgather_matches_torch_path_world1(gpu_ctx):
     assert native == via_torch == b"".join(k.tobytes() for k in kps)
 
 
-def test_gpu_cpp_batch_driver_world1(gpu_ctx):
+@pytest.mark.parametrize("n_gpus", [1, 2])
+def test_gpu_cpp_batch_driver(gpu_ctx, n_gpus):
     """tools/sift_batch_driver: images sharded i % n_gpus, one host thread
-    per GPU, records to HBM, native exchange; on one GPU every image's
-    record count and the exchanged bytes' word sum equal a direct detect's."""
+    per GPU, records to HBM, native exchange; every image's record count and
+    the exchanged bytes' word sum equal a direct detect's. With 2 GPUs (skipped
+    on a one-GPU box) the 3 images are uneven over the ranks (2 + 1), so the
+    padding to the largest rank and the rank-major compaction run for real."""
+    import torch
+
+    if torch.cuda.device_count() < n_gpus:
+        pytest.skip(f"needs {n_gpus} GPUs")
     exe = os.path.join(ROOT, "tools", "sift_batch_driver")
     assert os.path.exists(exe), "tools/sift_batch_driver not built (__graft_entry__.build())"
     w, h, n = 640, 480, 3
-    r = subprocess.run([exe, str(n), str(w), str(h), "1"], capture_output=True, text=True,
-                       timeout=120)
+    r = subprocess.run([exe, str(n), str(w), str(h), str(n_gpus)], capture_output=True,
+                       text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     kps = [gpu_ctx.detect(synth_image(w, h, 1, seed=42 + i))[0] for i in range(n)]
-    assert res["gpus"] == 1 and res["ranks_agree"]
+    assert res["gpus"] == n_gpus and res["ranks_agree"]
     assert res["counts"] == [len(k) for k in kps]
     words = np.frombuffer(b"".join(k.tobytes() for k in kps), dtype=np.uint64)
     assert res["total"] == sum(len(k) for k in kps)

@@ -6,7 +6,8 @@
 // image.cpp:156-214).
 //
 //   blur_lab VARIANT W H dec_at R1 R2 ...   (e.g. pc:1:64 3840 2160 2 4 5 6 8 10)
-// VARIANT = kind:C:rows, kind pc (tools/blur_variants.h) or strip (the
+// VARIANT = kind:C:rows, kind pc / ud (tools/blur_variants.h), pair (the
+// library's k_blur_pair at that shape) or strip (the
 // library's k_blur at that shape); the baseline is the library's launch_blur.
 //
 // Test tooling only: includes the library's kernel translation unit.

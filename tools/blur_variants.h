@@ -343,6 +343,14 @@ hipError_t launch_strip_r(const double* src, double* dst, int W, int H, int rows
     return launch_blur_r<R, C, kSrcPlane>(bsrc, dst, 0, 1, W, H, rows, t, dec, Wd, Hd, s, e0, e1);
 }
 
+// the library's pair walk (k_blur_pair) at an explicit shape
+template <int R, int C>
+hipError_t launch_pair_lab(const double* src, double* dst, int W, int H, int rows,
+                           const BlurTaps& t, double* dec, int Wd, int Hd, hipStream_t s,
+                           hipEvent_t e0, hipEvent_t e1) {
+    return launch_pair_r<R, C>(src, 0, dst, 0, 1, W, H, rows, t, dec, Wd, Hd, s, e0, e1);
+}
+
 using VarFn = hipError_t (*)(const double*, double*, int, int, int, const BlurTaps&, double*, int,
                              int, hipStream_t, hipEvent_t, hipEvent_t);
 
@@ -354,6 +362,8 @@ inline VarFn pick(const char* kind, int C, int R) {
     if (R == RR) {                                                                     \
         if (!std::strcmp(kind, "pc")) return C == 2 ? &launch_pc_r<RR, 2> : &launch_pc_r<RR, 1>; \
         if (!std::strcmp(kind, "ud")) return C == 2 ? &launch_ud_r<RR, 2> : &launch_ud_r<RR, 1>; \
+        if (!std::strcmp(kind, "pair"))                                                \
+            return C == 2 ? &launch_pair_lab<RR, 2> : &launch_pair_lab<RR, 1>;        \
         if (!std::strcmp(kind, "strip"))                                               \
             return C == 2 ? &launch_strip_r<RR, 2> : &launch_strip_r<RR, 1>;          \
     }

@@ -1,1 +1,1 @@
-bash tools/lab_session.sh r05_lab3 "ud:2:32 3840 2160 2 4 5 6 8 10" "ud:2:24 3840 2160 2 4 5 6 8 10" "ud:2:16 3840 2160 2 4 5 6 8 10" "ud:1:32 3840 2160 2 4 5 6 8 10" "ud:2:32 8192 8192 1 5 7 10 14" "ud:2:24 8192 8192 1 5 7 10 14" "ud:2:32 15360 8640 2 4 5 6 8 10" "ud:2:24 15360 8640 2 4 5 6 8 10" && bash tools/gpu_session.sh r05_l test bench timeline
+bash tools/gpu_session.sh r05_o test bench timeline && bash tools/bench_ab.sh r05_o/ab 3 base SIFT_HIP_LIB=sift-project_amd/alt/strip/libsift_hip.so

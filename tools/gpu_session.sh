@@ -6,6 +6,7 @@
 # prof   rocprofv3 --kernel-trace --stats of that same command, plus a
 #        serialised (SIFT_SERIAL=1, kernel-alone) trace; summaries via prof_summary.py
 # timeline  kernel trace of synchronous detects (the latency critical path)
+# apitrace  the same with the HIP runtime trace: launch call vs kernel start
 # steplog   the timed region's job timeline (bench.py --step-log)
 # ab/ab2/ab3  in-process interleaved A/B ($AB_ARGS ...); for anything that
 #        touches streams use tools/bench_ab.sh (one process per run)
@@ -61,6 +62,19 @@ for step in "$@"; do
     python tools/prof_summary.py $O/lat/run_kernel_trace.csv > $O/summary_lat.txt
     rm -rf $O/lat
     tail -45 $O/summary_lat.txt ;;
+  apitrace)
+    # host enqueue vs device execution of synchronous detects (HIP runtime
+    # trace joined with the kernel trace, tools/prof_api.py)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace \
+        --output-format csv -d $R/$O/api -o run \
+        -- python3 $R/bench.py --sync --steps 30 --warmup 5 --no-cpu-baseline --no-extra \
+        --no-matcher --no-alone --no-big --no-events > $R/$O/bench_api.json 2> $R/$O/bench_api.err \
+        || { tail -20 $R/$O/bench_api.err; exit 1; }
+    cd $R
+    python tools/prof_api.py $O/api > $O/api.txt 2>&1
+    rm -rf $O/api
+    head -80 $O/api.txt ;;
   steplog)
     # the driver's bench shape with the timed region's submit / fetch / done times
     timeout -k 10 120 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-matcher \

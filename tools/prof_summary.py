@@ -16,9 +16,12 @@ def main(path, n_images=None):
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
         tot[r["Kernel_Name"]] += d
         cnt[r["Kernel_Name"]] += 1
-    # one counter memset (fillBuffer) opens every detect; one k_job_done
-    # closes every pipelined / serialised job (the image count when present)
-    starts = [i for i, r in enumerate(rows) if "fillBuffer" in r["Kernel_Name"]]
+    # k_job_begin (a counter memset, fillBuffer, before round 5) opens every
+    # detect; one k_job_done closes every pipelined / serialised job (the
+    # image count when present)
+    starts = [i for i, r in enumerate(rows) if "k_job_begin" in r["Kernel_Name"]]
+    if not starts:
+        starts = [i for i, r in enumerate(rows) if "fillBuffer" in r["Kernel_Name"]]
     n_done = sum(1 for r in rows if "k_job_done" in r["Kernel_Name"])
     n_img = n_images or max(1, n_done or len(starts))
     print(f"{n_img} images")
@@ -37,9 +40,10 @@ def main(path, n_images=None):
             print(f"{f:12s} {c:9d} {t / n_img:9.1f} {t / c:14.2f}")
     if len(starts) >= 2:
         a, b = starts[-2], starts[-1]
-        # the image's first pyramid launch precedes its memset by a few dispatches
-        a = max(0, a - 2)
-        b = max(a + 1, b - 2)
+        # (the memset of earlier rounds came after the table upload)
+        if "fillBuffer" in rows[a]["Kernel_Name"]:
+            a = max(0, a - 2)
+            b = max(a + 1, b - 2)
         seg = rows[a:b]
         t0 = int(seg[0]["Start_Timestamp"])
         t1 = int(rows[b]["Start_Timestamp"])
