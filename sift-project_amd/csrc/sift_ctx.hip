@@ -773,7 +773,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         std::max<size_t>({s.exp_rec.cap, (size_t)8192 * n_img * kLanes, exp_hint});
     if ((st = s.exp_rec.ensure(exp_want)) != SIFT_OK ||
         (st = s.exp_side.ensure(s.exp_rec.cap)) != SIFT_OK ||
-        (st = s.exp_cnt.ensure(2 * (kMaxOctaves + 2))) != SIFT_OK)
+        (st = s.exp_cnt.ensure(kExportCntWords * (kMaxOctaves + 2))) != SIFT_OK)
         return st;
     // poison: a range no launch published reads as "not exported"
     std::fill(s.exp_cnt.h, s.exp_cnt.h + s.exp_cnt.cap, 0xFFFFFFFFu);
@@ -781,7 +781,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     s.exp_lane = s.exp_rec.cap / kLanes;
 
     auto run_chain = [&](int L, int o_begin, int o_end, const unsigned* cand_begin,
-                         unsigned* begin) -> int {
+                         unsigned* begin, hipStream_t sx) -> int {
         const int ci = s.n_chains++;
         s.chain_lane.push_back(L);
         while ((int)s.chain_ev.size() <= ci) {
@@ -790,11 +790,12 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 return SIFT_ERR_HIP;
             s.chain_ev.push_back(e);
         }
-        const ChainSpec c{L, o_begin, o_end, cand_begin, begin, lane_stream[L],
+        const ChainSpec c{L, o_begin, o_end, cand_begin, begin, sx,
                           s.d_ctr + kCtrWork + 4 * ci,
                           ExportSink{s.exp_rec.d + (size_t)L * s.exp_lane,
-                                     s.exp_side.d + (size_t)L * s.exp_lane, s.exp_cnt.d + 2 * ci,
-                                     (unsigned)s.exp_lane}};
+                                     s.exp_side.d + (size_t)L * s.exp_lane,
+                                     s.exp_cnt.d + kExportCntWords * ci, (unsigned)s.exp_lane,
+                                     s.d_ctr + 4 * L}};
         if ((st = enqueue_chain(ctx, s, c)) != SIFT_OK) return st;
         SIFT_HIP_TRY(hipEventRecord(s.chain_ev[ci], c.sx));
         return SIFT_OK;
@@ -805,14 +806,15 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     auto batch = [&](int o_begin, int o_end, std::initializer_list<hipStream_t> sps) -> int {
         const int gb = n_batches++;
         const int L = gb % lanes;
+        const hipStream_t sx = lane_stream[L];
         for (hipStream_t sp : sps) {
-            if (sp == lane_stream[L]) continue;  // same stream: already ordered
+            if (sp == sx) continue;  // same stream: already ordered
             hipEvent_t pyr_done = sync_event(s);
             if (!pyr_done) return SIFT_ERR_HIP;
             SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
-            SIFT_HIP_TRY(hipStreamWaitEvent(lane_stream[L], pyr_done, 0));
+            SIFT_HIP_TRY(hipStreamWaitEvent(sx, pyr_done, 0));
         }
-        return run_chain(L, o_begin, o_end, gb < lanes ? zeros : snap(gb - lanes), snap(gb));
+        return run_chain(L, o_begin, o_end, gb < lanes ? zeros : snap(gb - lanes), snap(gb), sx);
     };
     // Two pyramid streams (a job alone): the decimation chain on A — levels
     // 1 .. intervals of every octave, octave o+1 needs only level
@@ -854,11 +856,15 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         if (prof_events(ctx, s, &e0, &e1, bytes * n_img, SIFT_PROF_PYRAMID + o_small) != SIFT_OK)
             return SIFT_ERR_HIP;
         SIFT_HIP_TRY(launch_octaves_lds(d_pt, o_small, g.octaves - 1, g.n_gauss, s.d_stage->taps,
-                                        n_img, so, e0, e1));
+                                        n_img, g.W[o_small], g.H[o_small], so, e0, e1));
     }
+    // (the final batch of a job alone on stream A right behind k_octaves_lds,
+    // saving the lane stream's wait: synchronous latency +1.2 %, r05_s)
     if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
-    // lane D joins C, then the live counters come back on C: the job's last
-    // device work (the final batch waited on both pyramid streams)
+    // lane D joins C for the age counter (k_job_done): the job's last device
+    // work. The host does not wait for it: each lane's last descriptor launch
+    // publishes the lane's counters with its record range (ExportSink), so
+    // the job is complete on the host once its chains' events are.
     if (sD != sC) {
         hipEvent_t jd = sync_event(s);
         if (!jd) return SIFT_ERR_HIP;
@@ -869,8 +875,6 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         SIFT_HIP_TRY(launch_job_done(ctx->d_done, sC));
         s.job_done_enqueued = true;
     }
-    SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
-                                hipMemcpyDeviceToHost, sC));
     SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
     s.t_host[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     return SIFT_OK;
@@ -902,7 +906,8 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     };
     for (int ci = 0; ci < s.n_chains; ++ci) {
         SIFT_HIP_TRY(sync_ev(s.chain_ev[ci]));
-        const unsigned b = s.exp_cnt.h[2 * ci], e = s.exp_cnt.h[2 * ci + 1];
+        const unsigned* cnt = s.exp_cnt.h + kExportCntWords * ci;
+        const unsigned b = cnt[0], e = cnt[1];
         if (e > s.exp_lane || b > e) {
             s.exported = false;
             break;
@@ -915,7 +920,21 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     }
     s.run_start.push_back(s.n_keys);
 
-    // ---- the counters; re-run every candidate stage on overflow
+    // ---- the counters; re-run every candidate stage on overflow. Every
+    // chain has completed when its records were all exported: each lane's
+    // counters are those its last chain published. Otherwise (export
+    // overflow) they are copied back once the job's device work is done.
+    bool published = s.exported && s.n_chains > 0;
+    if (published) {
+        std::fill(s.h_ctr, s.h_ctr + 4 * kLanes, 0u);
+        for (int ci = 0; ci < s.n_chains; ++ci) {
+            const unsigned* cnt = s.exp_cnt.h + kExportCntWords * ci;
+            unsigned* h = s.h_ctr + 4 * s.chain_lane[ci];
+            h[0] = cnt[2];
+            h[1] = cnt[3];
+            h[2] = cnt[4];
+        }
+    }
     clk::time_point t_wait;
     for (int attempt = 0;; ++attempt) {
         if (attempt > 0) {
@@ -932,16 +951,18 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
                 unsigned* begin = s.d_ctr + kCtrSnap;
                 const ChainSpec c{0, 0, g.octaves, s.d_ctr + kCtrZeros, begin, sC,
                                   s.d_ctr + kCtrWork,
-                                  ExportSink{s.exp_rec.d, s.exp_side.d, nullptr, 0}};
+                                  ExportSink{s.exp_rec.d, s.exp_side.d, nullptr, 0, nullptr}};
                 s.n_chains = 1;
                 s.chain_lane.push_back(0);
                 if ((st = enqueue_chain(ctx, s, c)) != SIFT_OK) return st;
             }
+        }
+        if (attempt > 0 || !published) {
             SIFT_HIP_TRY(hipMemcpyAsync(s.h_ctr, s.d_ctr, 4 * kLanes * sizeof(unsigned),
                                         hipMemcpyDeviceToHost, sC));
             SIFT_HIP_TRY(hipEventRecord(s.done_ev, sC));
+            SIFT_HIP_TRY(sync_ev(s.done_ev));
         }
-        SIFT_HIP_TRY(sync_ev(s.done_ev));
         t_wait = clk::now();
         size_t nc = 0, nr = 0, no = 0;  // largest per-lane counts
         for (int L = 0; L < kLanes; ++L) {
@@ -1189,8 +1210,10 @@ void gather(Slot& s, sift_kp* out, float* df) {
     // record i's host row: exported -> lane-local index already offset by
     // host_base at export time (keep holds host positions); bulk -> concatenated
     // large outputs (config 5: 166 k records = 28 MB, much of it first
-    // touches of the caller's fresh pages) on the host pool's threads
-    constexpr size_t kPiece = 8192;
+    // touches of the caller's fresh pages) on the host pool's threads; the
+    // caller takes pieces too, so small outputs (1080p: ~6 k records, ~25 us
+    // alone) finish no later than on one thread
+    constexpr size_t kPiece = 512;
     const size_t n = s.n_final;
     const unsigned pieces = (unsigned)((n + kPiece - 1) / kPiece);
     auto copy = [&](unsigned t) {
@@ -1202,7 +1225,7 @@ void gather(Slot& s, sift_kp* out, float* df) {
                 std::memcpy(df + i * 128, s.h_df32.p + (size_t)s.keep[i] * 128,
                             128 * sizeof(float));
     };
-    if (pieces > 2) host_parallel(pieces, copy);
+    if (pieces > 1) host_parallel(pieces, copy);
     else
         for (unsigned t = 0; t < pieces; ++t) copy(t);
     s.t_host[4] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();

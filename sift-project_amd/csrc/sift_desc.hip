@@ -348,6 +348,9 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     if (ex.cnt && blockIdx.x == 0 && threadIdx.x == 0) {
         ex.cnt[0] = k0;
         ex.cnt[1] = n;
+        ex.cnt[2] = ex.live[0];  // the lane's final counters: extrema and
+        ex.cnt[3] = ex.live[1];  // refine and orientation of this chain
+        ex.cnt[4] = *n_rec;      // have completed (same stream)
     }
     if (threadIdx.x < 17) atab[threadIdx.x] = kAtanTab[threadIdx.x];
     // workgroup b's first record is b of the launch's range, the later ones

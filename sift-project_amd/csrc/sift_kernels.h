@@ -40,10 +40,16 @@ bool launch_blur_initial_fused(const double* in, size_t in_bs, int w, int h, int
                                double* dst, size_t bs, int n_img, int W0, int H0,
                                const BlurTaps& taps, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                                hipError_t* err);
-// every octave in [o_first, o_last] of every image (one workgroup per image)
+// every octave in [o_first, o_last] of every image (one workgroup per image;
+// octave o_first is W_first x H_first and must satisfy lds_octave_fits)
+struct LdsShape {
+    int cap, dcap;  // doubles of the level regions and of the next-base region
+    size_t bytes;   // dynamic LDS of the launch
+};
+LdsShape lds_shape(int W_first, int H_first, bool has_next, int n_gauss);
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
-                              const BlurTaps* d_taps, int n_img, hipStream_t s, hipEvent_t e0,
-                              hipEvent_t e1);
+                              const BlurTaps* d_taps, int n_img, int W_first, int H_first,
+                              hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // snap (optional): the last workgroup writes the lane counter snapshot
 // (candidate end, raw / record begins) for the keypoint chain; snap[3] must
 // be zero before the launch.

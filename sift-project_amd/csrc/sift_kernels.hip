@@ -865,11 +865,17 @@ struct LdsTables {
 // the kernel's body; `hook()` runs after the base load, every level and
 // every octave, `sub()` inside the tiny levels (no-ops here; tools/
 // lds_lab.hip stamps s_memtime there)
+// `cap` / `dcap`: doubles of the level regions (the first octave's level,
+// (W | 1) * H) and of the next-base region ((W / 2 | 1) * (H / 2)), so the
+// launch takes only the LDS its octaves need (1080p octaves 6-10: 37 KB) and
+// shares a CU with other workgroups instead of waiting for a whole CU's LDS
+// to drain (a job alone: up to ~35 us at dispatch beside its keypoint
+// chains, r05_s kernel trace)
 template <class Hook, class Sub = LdsNoHook>
 __device__ __forceinline__ void octaves_lds_run(const PyrTable* __restrict__ pt, int o_first,
                                                 int o_last, int n_gauss,
                                                 const BlurTaps* __restrict__ taps, double* lds,
-                                                Hook hook, Sub sub = Sub{}) {
+                                                int cap, int dcap, Hook hook, Sub sub = Sub{}) {
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
     const int dec_level = n_gauss - 3;
     const int b = blockIdx.x;                           // image of the job
@@ -888,9 +894,9 @@ __device__ __forceinline__ void octaves_lds_run(const PyrTable* __restrict__ pt,
     // in the quarter region D; the roles swap from octave to octave (the
     // next octave's levels fit in the quarter region), so no copy
     double* A = lds;                                    // current level
-    double* T = lds + kLdsOctavePx;                     // horizontal-pass temporary
-    double* D = lds + 2 * kLdsOctavePx;                 // next octave's base
-    double* const TP = lds + 2 * kLdsOctavePx + kLdsOctavePx / 4;  // staged taps
+    double* T = lds + cap;                              // horizontal-pass temporary
+    double* D = lds + 2 * cap;                          // next octave's base
+    double* const TP = lds + 2 * cap + dcap;            // staged taps
     for (int i = tid; i < n_gauss * kLdsTapStride; i += nt) {
         const int l = i / kLdsTapStride, j = i - l * kLdsTapStride;
         const BlurTaps& t = taps[l];
@@ -955,10 +961,11 @@ __device__ __forceinline__ void octaves_lds_run(const PyrTable* __restrict__ pt,
 
 __global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
                                                       int o_first, int o_last, int n_gauss,
-                                                      const BlurTaps* __restrict__ taps) {
+                                                      const BlurTaps* __restrict__ taps, int cap,
+                                                      int dcap) {
     set_job_prio(pt->jp, SIFT_PRIO_LDS);
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, LdsNoHook{});
+    octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, cap, dcap, LdsNoHook{});
 }
 
 // Generic fallbacks for kernels wider than kMaxTemplR (unusual sigmas): a
@@ -1914,11 +1921,21 @@ hipError_t prepare_kernel_attributes() {
                                (int)kLdsOctaveBytes);
 }
 
+LdsShape lds_shape(int W_first, int H_first, bool has_next, int n_gauss) {
+    LdsShape sh;
+    sh.cap = (((W_first | 1) * H_first) + 1) & ~1;  // even: 16-B aligned regions
+    sh.dcap = has_next ? ((((W_first / 2) | 1) * (H_first / 2)) + 1) & ~1 : 2;
+    sh.bytes = ((size_t)2 * sh.cap + sh.dcap + (size_t)n_gauss * kLdsTapStride) * sizeof(double);
+    return sh;
+}
+
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
-                              const BlurTaps* d_taps, int n_img, hipStream_t s, hipEvent_t e0,
-                              hipEvent_t e1) {
-    return launch_timed(k_octaves_lds, dim3(n_img), dim3(1024), kLdsOctaveBytes, s, e0, e1, d_pt,
-                        o_first, o_last, n_gauss, d_taps);
+                              const BlurTaps* d_taps, int n_img, int W_first, int H_first,
+                              hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (!lds_octave_fits(W_first, H_first) || n_gauss > kMaxLevels) return hipErrorInvalidValue;
+    const LdsShape sh = lds_shape(W_first, H_first, o_first < o_last, n_gauss);
+    return launch_timed(k_octaves_lds, dim3(n_img), dim3(1024), sh.bytes, s, e0, e1, d_pt,
+                        o_first, o_last, n_gauss, d_taps, sh.cap, sh.dcap);
 }
 
 hipError_t launch_prepare(const double* in, size_t in_bs, int w, int h, int c, int dbl,

@@ -153,12 +153,16 @@ struct GatherItem {
 // Where k_descriptor also writes each finished record (mapped, coherent
 // pinned host memory), so the host can finalise a keypoint batch while the
 // device works on the next: rec/side index = record index (< cap), cnt =
-// this launch's [begin, end) record range.
+// this launch's [begin, end) record range followed by the lane's live
+// counters (candidates, refined keypoints, records) read from `live`, so the
+// host has a job's counters when its last chains complete (no copy back).
+constexpr int kExportCntWords = 5;
 struct ExportSink {
     sift_kp* rec;
     RecSide* side;
     unsigned* cnt;
     unsigned cap;
+    const unsigned* live;  // the lane's counters (with cnt)
 };
 
 }  // namespace sift_amd

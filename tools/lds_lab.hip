@@ -49,7 +49,8 @@ __global__ __launch_bounds__(1024) void k_octaves_lds_stamped(const PyrTable* __
                                                               int n_gauss,
                                                               const BlurTaps* __restrict__ taps,
                                                               unsigned long long* stamps,
-                                                              unsigned long long* sub_stamps) {
+                                                              unsigned long long* sub_stamps,
+                                                              int cap, int dcap) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     int ns = 0;
     const Stamp st{stamps, &ns};
@@ -57,9 +58,9 @@ __global__ __launch_bounds__(1024) void k_octaves_lds_stamped(const PyrTable* __
     if (sub_stamps) {
         int ns2 = 0;
         const Stamp sub{sub_stamps, &ns2};
-        octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, st, sub);
+        octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, cap, dcap, st, sub);
     } else {
-        octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, st);
+        octaves_lds_run(pt, o_first, o_last, n_gauss, taps, lds, cap, dcap, st);
     }
 }
 
@@ -122,15 +123,18 @@ int main(int argc, char** argv) {
     CK(prepare_kernel_attributes());
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_octaves_lds_stamped),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsOctaveBytes));
+    const LdsShape sh = lds_shape(h.w[o_first], h.h[o_first], o_first < o_last, n_gauss);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const int reps = 50;
     for (int i = 0; i < 5; ++i)
-        CK(launch_octaves_lds(d_pt, o_first, o_last, n_gauss, d_taps, 1, 0, nullptr, nullptr));
+        CK(launch_octaves_lds(d_pt, o_first, o_last, n_gauss, d_taps, 1, h.w[o_first],
+                              h.h[o_first], 0, nullptr, nullptr));
     CK(hipEventRecord(e0, 0));
     for (int i = 0; i < reps; ++i)
-        CK(launch_octaves_lds(d_pt, o_first, o_last, n_gauss, d_taps, 1, 0, nullptr, nullptr));
+        CK(launch_octaves_lds(d_pt, o_first, o_last, n_gauss, d_taps, 1, h.w[o_first],
+                              h.h[o_first], 0, nullptr, nullptr));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -141,8 +145,8 @@ int main(int argc, char** argv) {
     std::vector<double> acc(kMaxStamps, 0.0);
     int n = 0;
     for (int r = 0; r < reps; ++r) {
-        hipLaunchKernelGGL(k_octaves_lds_stamped, dim3(1), dim3(1024), kLdsOctaveBytes, 0, d_pt,
-                           o_first, o_last, n_gauss, d_taps, d_st, nullptr);
+        hipLaunchKernelGGL(k_octaves_lds_stamped, dim3(1), dim3(1024), sh.bytes, 0, d_pt,
+                           o_first, o_last, n_gauss, d_taps, d_st, nullptr, sh.cap, sh.dcap);
         CK(hipGetLastError());
         CK(hipDeviceSynchronize());
         std::vector<unsigned long long> st(kMaxStamps);
@@ -165,8 +169,8 @@ int main(int argc, char** argv) {
     // phases inside the tiny levels: row pass, barrier, column pass, barrier
     std::vector<double> ph(4 * kMaxStamps, 0.0);
     for (int r = 0; r < reps; ++r) {
-        hipLaunchKernelGGL(k_octaves_lds_stamped, dim3(1), dim3(1024), kLdsOctaveBytes, 0, d_pt,
-                           o_first, o_last, n_gauss, d_taps, d_st, d_sub);
+        hipLaunchKernelGGL(k_octaves_lds_stamped, dim3(1), dim3(1024), sh.bytes, 0, d_pt,
+                           o_first, o_last, n_gauss, d_taps, d_st, d_sub, sh.cap, sh.dcap);
         CK(hipGetLastError());
         CK(hipDeviceSynchronize());
         std::vector<unsigned long long> st(kMaxStamps), su(kMaxStamps);
