@@ -807,10 +807,11 @@ def main() -> int:
         # profiles/) sits beside it
         roofline = chip_roofline(pyr_bytes_img, pyr_launches_img, images, elapsed,
                                  traffic.get("pyramid") if traffic else None, traffic_note)
-        roofline["kernel"] = ("Gaussian pyramid: k_blur (strip walk, octave 0 incl. the fused "
-                              "gray/x2 initial blur) + k_blur_tile (LDS tiles, octaves >= 1) + "
-                              "k_octaves_lds (LDS-resident small octaves); 16 B per pixel per "
-                              "level + 8 B per decimated pixel (SURVEY 8d)")
+        roofline["kernel"] = ("Gaussian pyramid: k_blur_pair (wave-pair walk, octave-0 levels "
+                              "1-5) + k_blur (strip walk: the fused gray/x2 initial blur) + "
+                              "k_blur_tile (LDS tiles, octaves >= 1) + k_octaves_lds "
+                              "(LDS-resident small octaves); 16 B per pixel per level + 8 B per "
+                              "decimated pixel (SURVEY 8d)")
         fp64_img = pyramid_fp64_ops(dims, params)
         roofline["fp64"] = {"ops_per_image": fp64_img, "peak_ops_per_s": FP64_PEAK_OPS,
                             "frac": fp64_img * images / elapsed / FP64_PEAK_OPS,

@@ -32,7 +32,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("config", choices=sorted(bench.BIG_CONFIGS))
     ap.add_argument("--images", type=int, default=12)
-    ap.add_argument("--depth", type=int, default=2)
+    ap.add_argument("--depth", type=int, default=bench.BIG_DEPTH)  # as the bench legs
     ap.add_argument("--warmup", type=int, default=-1,
                     help="warm-up jobs (default depth + 2: every slot the pipeline cycles "
                          "through has run one)")

@@ -1,1 +1,1 @@
-bash tools/gpu_session.sh r05_t test && bash tools/lds_session.sh r05_t lds_lab && timeout -k 10 400 python3 tools/kernel_alone.py --n 100 base base > gpurun_out/r05_t/alone.txt 2>&1 && grep -v amdgpu gpurun_out/r05_t/alone.txt && bash tools/gpu_session.sh r05_t timeline && bash tools/bench_ab.sh r05_t/ab 3 base SIFT_HIP_LIB=sift-project_amd/alt/strip/libsift_hip.so
+bash tools/gpu_session.sh r05_final3 big
