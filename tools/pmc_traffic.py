@@ -20,7 +20,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KNOWN = 96 * 2 ** 20 * 8  # bytes moved each way per calibration launch
-KERNEL_SOURCES = ("sift-project_amd/csrc/sift_kernels.hip", "sift-project_amd/csrc/sift_kernels.h",
+KERNEL_SOURCES = ("sift-project_amd/csrc/sift_kernels.hip", "sift-project_amd/csrc/sift_extrema.hip",
+                  "sift-project_amd/csrc/sift_kernels.h",
                   "sift-project_amd/csrc/sift_device.h", "sift-project_amd/csrc/sift_types.h")
 
 
