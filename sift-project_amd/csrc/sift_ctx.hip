@@ -54,7 +54,7 @@ namespace {
 using clk = std::chrono::steady_clock;
 
 constexpr unsigned kKpWgsMax = 512;               // keypoint workgroups per launch, at most
-constexpr unsigned kDescWgsAlone = 768;           // k_descriptor_split: 3 per CU resident
+constexpr unsigned kDescWgsAlone = 256u * SIFT_DSPLIT_OCC;  // k_descriptor_split: every resident slot
 constexpr size_t kTileMaxPx = (size_t)1 << 21;    // planes up to this size: LDS-tile blur
 
 // Keypoint lanes: batches alternate between two streams (C, D), each with

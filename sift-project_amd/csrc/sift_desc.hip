@@ -12,14 +12,6 @@
 #include "sift_kernels.h"
 #include "sift_math64.h"
 
-// replicas of the 4x4x8 f64 histogram per wave (power of two <= 16) and the
-// minimum workgroups per CU
-#ifndef SIFT_DSPLIT_REPS
-#define SIFT_DSPLIT_REPS 8
-#endif
-#ifndef SIFT_DSPLIT_OCC
-#define SIFT_DSPLIT_OCC (SIFT_DSPLIT_REPS >= 16 ? 2 : 3)
-#endif
 #ifndef SIFT_DESC_AHEAD  // steps of 64 samples whose gradient loads are in flight
 #define SIFT_DESC_AHEAD 1
 #endif

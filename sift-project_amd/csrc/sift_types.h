@@ -20,6 +20,18 @@ constexpr int kDescBins = 8;        // DESC_HIST_BINS
 constexpr double kMagThr = 0.2;     // DESC_MAGNITUDE_THR
 constexpr double kIntFactor = 512.0;  // INT_DESCR_FCTR
 
+// k_descriptor_split: replicas of the 4x4x8 f64 histogram per wave (power
+// of two <= 16) and the waves per SIMD it is compiled for (= workgroups of
+// 4 waves per CU; the host sizes a chip-filling grid from it). 4: 128 VGPRs
+// with 6 spilled outside the sample loop, 4 x 39 KB of LDS per CU; against
+// 3 (149 VGPRs): alone 156 -> 152.5 us per 1080p image, the driver's
+// command -1.7 % (r05_v)
+#ifndef SIFT_DSPLIT_REPS
+#define SIFT_DSPLIT_REPS 8
+#endif
+#ifndef SIFT_DSPLIT_OCC
+#define SIFT_DSPLIT_OCC (SIFT_DSPLIT_REPS >= 16 ? 2 : 4)
+#endif
 constexpr int kMaxOctaves = 16;   // floor(log2(min/3)) < 16 for any int image
 constexpr int kOctBits = 4;       // sift_extremum.octave = o | image << kOctBits
 constexpr int kMaxImages = 16;    // images of one job (one batched launch each)
