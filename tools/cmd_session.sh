@@ -1,1 +1,1 @@
-mkdir -p gpurun_out/r05_v && SIFT_HIP_LIB=sift-project_amd/alt/occ4/libsift_hip.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_v/pytest_occ4.log 2>&1 && tail -1 gpurun_out/r05_v/pytest_occ4.log && timeout -k 10 400 python3 tools/kernel_alone.py --n 100 base SIFT_HIP_LIB=sift-project_amd/alt/occ4/libsift_hip.so base SIFT_HIP_LIB=sift-project_amd/alt/occ4/libsift_hip.so > gpurun_out/r05_v/alone.txt 2>&1 && grep -v amdgpu gpurun_out/r05_v/alone.txt && bash tools/bench_ab.sh r05_v/ab 3 base SIFT_HIP_LIB=sift-project_amd/alt/occ4/libsift_hip.so
+bash tools/gpu_session.sh r05_final6 bench prof big
