@@ -54,6 +54,10 @@ namespace {
 using clk = std::chrono::steady_clock;
 
 constexpr unsigned kKpWgsMax = 512;               // keypoint workgroups per launch, at most
+// k_orient_wave with nothing beside it: every resident slot (4 workgroups
+// per CU); against 512: alone 50.7 -> 46.0 us per 1080p image, configs 3 / 5
+// orientation -16 / -18 % (r05_w, r05_final)
+constexpr unsigned kOriWgsAlone = 1024;
 constexpr unsigned kDescWgsAlone = 256u * SIFT_DSPLIT_OCC;  // k_descriptor_split: every resident slot
 constexpr size_t kTileMaxPx = (size_t)1 << 21;    // planes up to this size: LDS-tile blur
 
@@ -545,7 +549,7 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
     // 0.86 vs 0.82-0.84 ms, profiles/r04_final/summary_lat.txt)
     const bool alone = ctx->serial || (s.lanes > 1 && o_end == g.octaves);
     const unsigned ori_wgs =
-        alone ? kKpWgsMax : std::min(kKpWgsMax, ctx->kp_wgs * (unsigned)n_img);
+        alone ? kOriWgsAlone : std::min(kKpWgsMax, ctx->kp_wgs * (unsigned)n_img);
     const unsigned desc_wgs =
         alone ? kDescWgsAlone : std::min(kKpWgsMax, ctx->desc_wgs * (unsigned)n_img);
     hipEvent_t r0, r1, q0, q1, d0, d1;  // profiling events of the keypoint stages
