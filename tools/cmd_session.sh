@@ -1,1 +1,1 @@
-mkdir -p gpurun_out/r05_final8 && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/r05_final8/smoke.log 2>&1 && tail -2 gpurun_out/r05_final8/smoke.log && bash tools/pmc_session.sh r05_final8 && python3 tools/pmc_traffic.py gpurun_out/r05_final8 gpurun_out/r05_final8/traffic.json && cp gpurun_out/r05_final8/traffic.json profiles/traffic.json && rm -rf gpurun_out/r05_final8/calib_* gpurun_out/r05_final8/bench_FETCH_SIZE gpurun_out/r05_final8/bench_WRITE_SIZE && bash tools/gpu_session.sh r05_final8 test bench prof timeline
+bash tools/gpu_session.sh r05_check test bench
