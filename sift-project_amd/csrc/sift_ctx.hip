@@ -380,7 +380,13 @@ bool debug_enabled() {
     return on;
 }
 
-#define SIFT_HIP_TRY(expr)                                                              \
+// a keypoint batch of a job alone waits only on the tail stream (B), whose
+// join with A already orders the octave's chain levels (0: both streams)
+#ifndef SIFT_TAIL_JOIN_ONLY
+#define SIFT_TAIL_JOIN_ONLY 1
+#endif
+
+#define SIFT_HIP_TRY(expr)                                                            \
     do {                                                                                \
         hipError_t e_ = (expr);                                                         \
         if (e_ != hipSuccess) {                                                         \
@@ -847,7 +853,11 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, two_pyr ? sB : sA));
             ctx->pyr_last = (int)(&s - ctx->slots);
         }
-        if (o < o_merge && (st = batch(o, o + 1, {sA, sB})) != SIFT_OK) return st;
+        // two pyramid streams: B joined A before the octave's tail levels, so
+        // an event after them on B covers the whole octave; one join, not two
+        if (o < o_merge && (st = (two_pyr && SIFT_TAIL_JOIN_ONLY) ? batch(o, o + 1, {sB})
+                                                                   : batch(o, o + 1, {sA, sB})))
+            return st;
     }
     if (o_small < g.octaves) {  // on the chain stream, after the last decimation
         hipStream_t so = sA;

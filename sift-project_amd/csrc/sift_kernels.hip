@@ -716,6 +716,14 @@ constexpr int kLdsRun = 4;
 #define SIFT_LDS_TINY_PX 600
 #endif
 constexpr int kLdsTinyPx = SIFT_LDS_TINY_PX;
+// threads of k_octaves_lds: with ~120 VGPRs a wave, 1024 threads (4 waves
+// per SIMD) take a CU's whole register file, so the launch waited at
+// dispatch for a CU with no other wave resident (~25 us beside a job's
+// keypoint chains); 512 take half of it: 34 -> 36 us alone, synchronous
+// latency -1.2 %, pipelined step +-0 (r05_l512)
+#ifndef SIFT_LDS_THREADS
+#define SIFT_LDS_THREADS 512
+#endif
 
 template <int R>
 __device__ void lds_level(const LdsLevel& L, const double* __restrict__ tp) {
@@ -823,9 +831,9 @@ __device__ void lds_level_tiny(const LdsLevel& L, const double* __restrict__ tp,
 // kernels wider than kMaxTemplR (unusual sigmas): runtime radius, taps and
 // IEEE division from the global table
 __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int W = L.W, H = L.H, R = t.R, P = L.P;
-    for (int y = ty; y < H; y += 16) {
+    for (int y = ty; y < H; y += nw) {
         const double* row = L.A + y * P;
         for (int x = tx; x < W; x += 64) {
             double acc = row[x] * t.k[0];
@@ -834,7 +842,7 @@ __device__ void lds_level_any(const LdsLevel& L, const BlurTaps& t) {
         }
     }
     __syncthreads();
-    for (int y = ty; y < H; y += 16) {
+    for (int y = ty; y < H; y += nw) {
         for (int x = tx; x < W; x += 64) {
             double acc = L.T[y * P + x] * t.k[0];
             for (int u = 1; u <= R; ++u)
@@ -942,8 +950,8 @@ __device__ __forceinline__ void octaves_lds_run(const PyrTable* __restrict__ pt,
                 SIFT_LDS_CASE(9) SIFT_LDS_CASE(10) SIFT_LDS_CASE(11) SIFT_LDS_CASE(12)
 #undef SIFT_LDS_CASE
                 default:  // R > 12 (intervals <= 2, larger sigmas): templated
-                          // radii beyond 12 would push the 1024-thread kernel
-                          // past 128 VGPRs into scratch
+                          // radii beyond 12 would push the kernel past 128
+                          // VGPRs into scratch
                     lds_level_any(L, taps[l]);
             }
             hook();
@@ -956,7 +964,7 @@ __device__ __forceinline__ void octaves_lds_run(const PyrTable* __restrict__ pt,
     }
 }
 
-__global__ __launch_bounds__(1024) void k_octaves_lds(const PyrTable* __restrict__ pt,
+__global__ __launch_bounds__(SIFT_LDS_THREADS) void k_octaves_lds(const PyrTable* __restrict__ pt,
                                                       int o_first, int o_last, int n_gauss,
                                                       const BlurTaps* __restrict__ taps, int cap,
                                                       int dcap) {
@@ -1691,7 +1699,7 @@ hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int
                               hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (!lds_octave_fits(W_first, H_first) || n_gauss > kMaxLevels) return hipErrorInvalidValue;
     const LdsShape sh = lds_shape(W_first, H_first, o_first < o_last, n_gauss);
-    return launch_timed(k_octaves_lds, dim3(n_img), dim3(1024), sh.bytes, s, e0, e1, d_pt,
+    return launch_timed(k_octaves_lds, dim3(n_img), dim3(SIFT_LDS_THREADS), sh.bytes, s, e0, e1, d_pt,
                         o_first, o_last, n_gauss, d_taps, sh.cap, sh.dcap);
 }
 
