@@ -339,6 +339,20 @@ def pyramid_fp64_ops(octave_dims, params) -> float:
     return float(ops)
 
 
+def survey_bpyr(octave_dims, params) -> float:
+    """SURVEY 8d's B_pyr of one image: sum over octaves of (G-1) * 16 * N_o,
+    plus 8 * N_{o+1} per decimation; the initial blur is not counted (config
+    2: 884.7 MB). The headline's bytes also charge the fused initial blur at
+    its real I/O; both fractions are reported."""
+    G = params.intervals + 3
+    b = 0.0
+    for o, (w, h) in enumerate(octave_dims):
+        b += (G - 1) * 16.0 * w * h
+        if o + 1 < len(octave_dims):
+            b += 8.0 * octave_dims[o + 1][0] * octave_dims[o + 1][1]
+    return b
+
+
 def _rows_roofline(prof, n_images):
     """Kernel-alone figures from dispatch-timestamped events (SIFT_SERIAL
     context: every kernel alone on the chip)."""
@@ -812,6 +826,9 @@ def main() -> int:
                               "k_blur_tile (LDS tiles, octaves >= 1) + k_octaves_lds "
                               "(LDS-resident small octaves); 16 B per pixel per level + 8 B per "
                               "decimated pixel (SURVEY 8d)")
+        bpyr = survey_bpyr(dims, params)
+        roofline["survey_bpyr_bytes_per_image"] = bpyr
+        roofline["frac_survey_bpyr"] = round(bpyr * images / elapsed / 1e9 / HBM_PEAK_GBS, 4)
         fp64_img = pyramid_fp64_ops(dims, params)
         roofline["fp64"] = {"ops_per_image": fp64_img, "peak_ops_per_s": FP64_PEAK_OPS,
                             "frac": fp64_img * images / elapsed / FP64_PEAK_OPS,
@@ -897,6 +914,27 @@ def main() -> int:
             kps_a, _ = ctx.detect_device(dev_imgs[0].data_ptr(), W, H, 1, params)
             out["matcher"] = matcher_bench(ctx, dev, kps_a, W, H, params,
                                            0.0 if args.no_cpu_baseline else args.cpu_seconds)
+        # the headline figures again, last, so a tail of the line carries them
+        summ = {"keypoints_per_s": out["value"], "ms_per_step": out["ms_per_step"],
+                "pyramid_frac_chip": roofline["frac"],
+                "pyramid_frac_chip_survey_bpyr": roofline["frac_survey_bpyr"]}
+        if "alone" in roofline:
+            summ["pyramid_frac_alone"] = roofline["alone"]["frac"]
+            summ["pyramid_us_alone"] = roofline["alone"]["us_per_image"]
+            summ["extrema_frac_alone"] = extrema_roofline["alone"]["frac"]
+        if "keypoint_kernels_alone" in out:
+            summ["keypoint_kernels_us_alone"] = {
+                k: v.get("us_per_image") for k, v in out["keypoint_kernels_alone"].items()
+                if isinstance(v, dict)}
+        if "latency" in out:
+            summ["latency_ms_per_image"] = out["latency"]["ms_per_image"]
+        for name in ("config3", "config5"):
+            if name in out:
+                summ[f"{name}_ms_per_image"] = out[name]["ms_per_image"]
+                summ[f"{name}_pyramid_frac_alone"] = out[name]["roofline"]["alone"]["frac"]
+        if "cpu_baseline_reference" in out:
+            summ["x_reference_cpu_1core"] = out["value"] / out["cpu_baseline_reference"]["value"]
+        out["summary"] = summ
         print(json.dumps(out), file=json_out, flush=True)
 
     ctx.close()

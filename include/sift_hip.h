@@ -144,6 +144,10 @@ const char* sift_hip_strerror(int status);
  * Host double images whose values are all integers 0..255 (every
  * stb-decoded Image) are uploaded as bytes; the results are identical.
  * Device / host input buffers must stay valid until sift_hip_wait returns.
+ * Pixel values must be finite (the reference's loader only produces 0..255):
+ * host double images holding a NaN or an infinity are rejected with
+ * SIFT_ERR_ARG; device double images are not scanned, and such values give
+ * unspecified keypoints.
  */
 #define SIFT_INPUT_F64_HOST 0
 #define SIFT_INPUT_F64_DEVICE 1

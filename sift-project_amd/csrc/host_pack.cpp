@@ -11,6 +11,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -177,6 +178,27 @@ bool host_pack_u8(const double* src, size_t n, uint8_t* dst) {
         const size_t b = (size_t)t * kChunk, e = std::min(n, b + kChunk);
         ok[t] = pack_range(src + b, e - b, dst + b);
     });
+    for (char c : ok)
+        if (!c) return false;
+    return true;
+}
+
+bool host_copy_finite(const double* src, size_t n, double* dst) {
+    const size_t kChunk = (size_t)1 << 17;
+    const unsigned tasks = (unsigned)((n + kChunk - 1) / kChunk);
+    std::vector<char> ok(std::max(tasks, 1u), 1);
+    auto part = [&](unsigned t) {
+        const size_t b = (size_t)t * kChunk, e = std::min(n, b + kChunk);
+        std::memcpy(dst + b, src + b, (e - b) * sizeof(double));
+        bool fin = true;
+        for (size_t i = b; i < e; ++i) fin &= std::isfinite(src[i]);
+        ok[t] = fin;
+    };
+    if (tasks <= 1) {
+        if (n) part(0);
+    } else {
+        pool().run(tasks, part);
+    }
     for (char c : ok)
         if (!c) return false;
     return true;

@@ -68,6 +68,7 @@ struct sift_comm {
     // device send (kWordCap) + gathered (kWordCap * nranks), pinned host same
     int64_t* d_words = nullptr;
     int64_t* h_words = nullptr;
+    int64_t seq = 0;  // exchange calls so far (sift_exchange.h tags)
     // grow-only payload scratch: one send slot + nranks receive slots
     unsigned char* d_send = nullptr;
     unsigned char* d_recv = nullptr;
@@ -94,6 +95,13 @@ int comm_create(int device, int nranks, sift_comm** out) {
         sift_hip_comm_destroy(c);
         return SIFT_ERR_NOMEM;
     }
+    // no valid tag in the send words before the first call (a staging
+    // failure in that call then shows as tag 0 to the peers)
+    if (hipMemset(c->d_words, 0, words * sizeof(int64_t)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+        sift_hip_comm_destroy(c);
+        return SIFT_ERR_HIP;
+    }
     *out = c;
     return SIFT_OK;
 }
@@ -104,24 +112,25 @@ struct RcclTransport {
     hipStream_t st;
     int rank() const { return c->rank; }
     int nranks() const { return c->nranks; }
-    int gather_words(const int64_t* mine, int64_t* all, size_t words) {
-        if (words > kWordCap) return SIFT_ERR_ARG;
+    int64_t next_seq() { return ++c->seq; }
+    int gather_words(const int64_t* mine, int64_t* all, size_t words, bool* sent) {
+        if (words > kWordCap) return SIFT_ERR_NO_COMM;  // equal on every rank: no collective
         std::memcpy(c->h_words, mine, words * sizeof(int64_t));
         // a failed staging copy still joins the collective (the peers are
-        // in it); its status travels in the words the caller checks next
-        const bool staged = hipMemcpyAsync(c->d_words, c->h_words, words * sizeof(int64_t),
-                                           hipMemcpyHostToDevice, st) == hipSuccess;
+        // in it): they receive the send buffer's previous words, whose tag
+        // is not this call's, and count this rank as failed
+        *sent = hipMemcpyAsync(c->d_words, c->h_words, words * sizeof(int64_t),
+                               hipMemcpyHostToDevice, st) == hipSuccess;
         if (rccl().all_gather(c->d_words, c->d_words + kWordCap, words, ncclInt64, c->comm,
                               st) != ncclSuccess)
             return SIFT_ERR_NO_COMM;
-        if (!staged ||
-            hipMemcpyAsync(c->h_words + kWordCap, c->d_words + kWordCap,
+        if (hipMemcpyAsync(c->h_words + kWordCap, c->d_words + kWordCap,
                            words * c->nranks * sizeof(int64_t), hipMemcpyDeviceToHost,
                            st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return SIFT_ERR_HIP;
         std::memcpy(all, c->h_words + kWordCap, words * c->nranks * sizeof(int64_t));
-        return SIFT_OK;
+        return *sent ? SIFT_OK : SIFT_ERR_HIP;
     }
     int reserve(size_t slot, unsigned char** d_send, unsigned char** d_recv) {
         if (slot > c->slot_cap) {

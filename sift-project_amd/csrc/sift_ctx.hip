@@ -577,6 +577,32 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
 // ---------------------------------------------------------------------------
 // enqueue one job on slot s (everything up to the counter read-back)
 // ---------------------------------------------------------------------------
+
+// The mapped export buffers (records written by the descriptor kernel
+// straight into host memory) are an optimisation: a job whose records do
+// not fit takes one bulk download instead. So their size is capped, and a
+// failed allocation falls back to the minimum, then to no buffer at all,
+// rather than failing the job (the hint is the context-wide largest
+// records-per-pixel seen, which one dense image can make large).
+constexpr size_t kExportMaxRecs = (size_t)1 << 22;  // both lanes: 704 MB + sides
+void grow_export(Slot& s, double want, size_t min_want) {
+    const size_t w = (size_t)std::min<double>(want, (double)kExportMaxRecs);
+    const size_t m = std::min(min_want, kExportMaxRecs);
+    if (s.exp_rec.cap >= std::max(w, m) && s.exp_side.cap >= s.exp_rec.cap) {
+        s.exp_lane = s.exp_rec.cap / kLanes;
+        return;
+    }
+    for (size_t n : {std::max(w, m), m}) {
+        if (s.exp_rec.ensure(n) == SIFT_OK && s.exp_side.ensure(s.exp_rec.cap) == SIFT_OK) {
+            s.exp_lane = s.exp_rec.cap / kLanes;
+            return;
+        }
+        s.exp_rec.release();
+        s.exp_side.release();
+    }
+    s.exp_lane = 0;
+}
+
 int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     const auto t0 = clk::now();
     s.t_submit = t0;
@@ -621,10 +647,15 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 for (int b = 0; b < n_img && as_u8; ++b)
                     as_u8 = host_pack_u8(static_cast<const double*>(images[b]), ne,
                                          s.h_up.p + b * ne);
+                // other doubles go up as they are, and must be finite: the
+                // extrema scan is built without NaN semantics (Makefile
+                // EXT_FLAGS) and the reference's image loader never produces
+                // NaN / Inf (image_io.cpp:20-35)
                 if (!as_u8)
                     for (int b = 0; b < n_img; ++b)
-                        std::memcpy(s.h_up.p + b * ne * sizeof(double), images[b],
-                                    ne * sizeof(double));
+                        if (!host_copy_finite(static_cast<const double*>(images[b]), ne,
+                                              reinterpret_cast<double*>(s.h_up.p) + b * ne))
+                            return SIFT_ERR_ARG;
             }
             if (as_u8) {
                 if ((st = s.in8.ensure(ne * n_img)) != SIFT_OK) return st;
@@ -719,8 +750,12 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     const int W0 = g.W[0], H0 = g.H[0];
     {
         hipEvent_t e0, e1;
-        if (prof_events(ctx, s, &e0, &e1, 16.0 * n_img * (double)W0 * H0, SIFT_PROF_PYRAMID) !=
-            SIFT_OK)
+        // the fused initial blur's real I/O: the input image read once (8 B
+        // per value) and G[0][0] written once (not 16 B per
+        // output pixel)
+        const double init_bytes =
+            n_img * (8.0 * (double)s.w * (double)s.h * s.c + 8.0 * (double)W0 * H0);
+        if (prof_events(ctx, s, &e0, &e1, init_bytes, SIFT_PROF_PYRAMID) != SIFT_OK)
             return SIFT_ERR_HIP;
         hipError_t err = hipSuccess;
         const bool fused = launch_blur_initial_fused(src, in_bs, s.w, s.h, s.c,
@@ -777,14 +812,10 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // records of every chain also go to the mapped export buffers, sized from
     // the largest record count seen so far (a larger one falls back to one
     // bulk download at the end, and grows them for the next call)
-    const size_t exp_hint =
-        (size_t)(ctx->exp_px_hint * 1.5 * (double)W0 * (double)H0 * n_img) * kLanes;
-    const size_t exp_want =
-        std::max<size_t>({s.exp_rec.cap, (size_t)8192 * n_img * kLanes, exp_hint});
-    if ((st = s.exp_rec.ensure(exp_want)) != SIFT_OK ||
-        (st = s.exp_side.ensure(s.exp_rec.cap)) != SIFT_OK ||
-        (st = s.exp_cnt.ensure(kExportCntWords * (kMaxOctaves + 2))) != SIFT_OK)
-        return st;
+    const double exp_hint =
+        ctx->exp_px_hint * 1.5 * (double)W0 * (double)H0 * n_img * kLanes;
+    grow_export(s, std::max<double>(exp_hint, (double)s.exp_rec.cap), (size_t)8192 * n_img * kLanes);
+    if ((st = s.exp_cnt.ensure(kExportCntWords * (kMaxOctaves + 2))) != SIFT_OK) return st;
     // poison: a range no launch published reads as "not exported"
     std::fill(s.exp_cnt.h, s.exp_cnt.h + s.exp_cnt.cap, 0xFFFFFFFFu);
     // lane L exports its records (lane-local index i) to exp_rec[L * exp_lane + i]
@@ -907,7 +938,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     const sift_params* p = &s.p;
     int st;
     hipStream_t sC = s.sC;
-    s.exported = true;
+    s.exported = s.exp_lane > 0;  // no export buffer: the bulk path
     s.n_keys = 0;
     s.run_start.clear();
     s.fin_ws.all.resize(s.exp_rec.cap);
@@ -1067,12 +1098,8 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
                                   s.img_count.data(), &s.fin_ws);
         // the next job in this slot exports this many records per lane
         const unsigned lane_max = std::max(s.n_lane[0], s.n_lane[1]);
-        if (lane_max > s.exp_lane) {
-            const size_t want = ((size_t)lane_max + lane_max / 2) * kLanes;
-            if ((st = s.exp_rec.ensure(want)) != SIFT_OK ||
-                (st = s.exp_side.ensure(want)) != SIFT_OK)
-                return st;
-        }
+        if (lane_max > s.exp_lane)
+            grow_export(s, ((double)lane_max + lane_max / 2) * kLanes, (size_t)8192 * s.n_img * kLanes);
     }
     const auto t_fin = clk::now();
     s.t_host[1] = ms(t0, t_wait);

@@ -15,6 +15,9 @@
 #ifndef SIFT_DESC_AHEAD  // steps of 64 samples whose gradient loads are in flight
 #define SIFT_DESC_AHEAD 1
 #endif
+#ifndef SIFT_DESC_SWZ  // replica swizzle of the histogram bins (hist_slot)
+#define SIFT_DESC_SWZ 2
+#endif
 
 namespace sift_amd {
 
@@ -71,9 +74,28 @@ __device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevP
     return d;
 }
 
+// LDS slot of bin i of replica r in a wave's NR lane-interleaved replicas.
+// Unswizzled (bin i at i * NR + r) the lanes that share a replica map onto
+// the same banks whenever their bins agree modulo 32 / NR, and neighbouring
+// samples mostly differ only in their spatial cell (i = row_bin * 32 +
+// col_bin * 8 + ori_bin): 45 % of the descriptor's LDS cycles were bank
+// conflicts (round 5). XOR-ing the replica index with bits of the cell moves
+// neighbouring cells to other banks. It only relocates the slot: the adds
+// into a given (replica, bin) and their order are unchanged, so every
+// histogram is bit-identical.
+template <int NR>
+__device__ __forceinline__ int hist_slot(int i, int r) {
+    int f = 0;
+    if (SIFT_DESC_SWZ == 1) f = i >> 2;                                // ori bit 2, col_bin
+    if (SIFT_DESC_SWZ == 2) f = ((i >> 3) & 3) | (((i >> 5) & 1) << 2);  // col_bin, row_bin bit 0
+    if (SIFT_DESC_SWZ == 3) f = i >> 1;
+    return i * NR + (r ^ (f & (NR - 1)));
+}
+
 // ---------------------------------------------------------------------------
 // One sample (col, row) with gradient loads cv = I(x+1), I(x-1), I(y-1),
-// I(y+1) into this lane's replica `rep` (bin i at rep[i * NR]).
+// I(y+1) into this lane's replica r of the wave's histograms `hist`
+// (bin i at hist[hist_slot(i, r)]).
 // The reference's expressions (sift.cpp:641-678): row_rot / col_rot
 // with the correctly rounded division by hist_width, (row_rot + 2) - 0.5,
 // sqrt, atan2 - pori and the two fmods (exact compare-and-subtract),
@@ -84,7 +106,7 @@ __device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevP
 // (row_bin = -1 exactly), so the contributing sample set is the reference's.
 // ---------------------------------------------------------------------------
 template <int NR>
-__device__ __forceinline__ void add_sample_f64(double* rep, int scol, int srow, const double* cv,
+__device__ __forceinline__ void add_sample_f64(double* hist, int r, int scol, int srow, const double* cv,
                                                const DescRecord& d, const double2* atab,
                                                const double* gtab) {
     constexpr double kBinsPerRad = kDescBins / kTwoPi;  // sift.cpp:628
@@ -126,9 +148,9 @@ __device__ __forceinline__ void add_sample_f64(double* rep, int scol, int srow, 
             const int ci = bc + cq;
             if ((unsigned)ci >= (unsigned)kDescW) continue;
             const double vc = vr * ((cq == 0) ? 1.0 - fc : fc);
-            double* hb = &rep[(ri * 32 + ci * 8) * NR];
-            atomicAdd(&hb[(bo & 7) * NR], vc * (1.0 - fo));
-            atomicAdd(&hb[((bo + 1) & 7) * NR], vc * fo);
+            const int cell = ri * 32 + ci * 8;
+            atomicAdd(&hist[hist_slot<NR>(cell + (bo & 7), r)], vc * (1.0 - fo));
+            atomicAdd(&hist[hist_slot<NR>(cell + ((bo + 1) & 7), r)], vc * fo);
         }
     }
 }
@@ -149,7 +171,7 @@ __device__ __forceinline__ void add_sample_f64(double* rep, int scol, int srow, 
 //    can count them).
 // ---------------------------------------------------------------------------
 template <int NR>
-__device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, double* rep,
+__device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, double* hist,
                                           const double2* atab, const double* gtab) {
     const int lane = threadIdx.x & 63;
     const int side = 2 * d.radius + 1;
@@ -225,7 +247,8 @@ __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, d
             qrow[A] = qcol[A] = 0;
             qok[A] = t0 + 64 * A < total && locate(t0 + 64 * A, qrow[A], qcol[A]);
             fetch(qok[A], qrow[A], qcol[A], qv[A]);
-            if (qok[0]) add_sample_f64<NR>(rep, qcol[0], qrow[0], qv[0], d, atab, gtab);
+            if (qok[0])
+                add_sample_f64<NR>(hist, lane & (NR - 1), qcol[0], qrow[0], qv[0], d, atab, gtab);
 #pragma unroll
             for (int a = 0; a < A; ++a) {
                 qrow[a] = qrow[a + 1];
@@ -238,7 +261,7 @@ __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, d
     }
 }
 
-// This wave's NR replicas (bin i of replica r at hist[i * NR + r]) -> bins
+// This wave's NR replicas (bin i of replica r at hist[hist_slot(i, r)]) -> bins
 // lane and lane + 64, in a fixed order per bin (rotated by lane so the 16
 // lanes of a read group start on different bank pairs)
 template <int NR>
@@ -248,8 +271,8 @@ __device__ __forceinline__ void reduce_replicas(const double* hist, double& v0, 
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
         const int r = (q + lane) & (NR - 1);
-        v0 += hist[lane * NR + r];
-        v1 += hist[(lane + 64) * NR + r];
+        v0 += hist[hist_slot<NR>(lane, r)];
+        v1 += hist[hist_slot<NR>(lane + 64, r)];
     }
 }
 
@@ -332,7 +355,6 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double* const hist = hist_all + wv * 128 * kSplitReps;
-    double* const rep = hist + (lane & (kSplitReps - 1));
     const unsigned n = min(*n_rec, cap_rec);
     const unsigned k0 = min(*rec_begin, n);
     // the launch's record range is fixed before it starts (orientation has
@@ -372,7 +394,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
         for (int i = lane; i < 64 * kSplitReps; i += 64)
             reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
         __syncthreads();  // the table (uniform: every thread gets here)
-        desc_walk<kSplitReps>(d, wv, 4, rep, atab, use_tab ? gtab : nullptr);
+        desc_walk<kSplitReps>(d, wv, 4, hist, atab, use_tab ? gtab : nullptr);
         wave_sync();
         double v0, v1;
         reduce_replicas<kSplitReps>(hist, v0, v1);

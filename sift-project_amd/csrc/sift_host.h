@@ -61,6 +61,8 @@ size_t host_finalize(const sift_params* p, sift_kp* recs, const RecSide* side, u
 // is what an stb-decoded Image holds (image_io.cpp:20-35); returns false
 // (dst unspecified) otherwise.
 bool host_pack_u8(const double* src, size_t n, uint8_t* dst);
+// copies n doubles (host pool); false when any of them is NaN or infinite
+bool host_copy_finite(const double* src, size_t n, double* dst);
 
 // fn(t) for t in [0, n_tasks) on the same persistent host threads (the
 // caller included); returns when all are done

@@ -58,7 +58,6 @@ ERRORS = {
     -8: "invalid call order (no such job / no previous detect / too many jobs in flight)",
     -9: "RCCL unavailable or a collective failed",
     -10: "another rank of the collective failed",
-    -10: "another rank of the collective failed",
 }
 
 # exported symbols declared in include/sift_hip.h

@@ -243,9 +243,11 @@ def test_bench_gpus_n_launches_one_worker_per_gpu():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    # (small and without the extra legs: on a multi-GPU box the workers run)
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
-                        "1", "--warmup", "1"], capture_output=True, text=True, timeout=300,
-                       env=env)
+                        "1", "--warmup", "1", "--no-big", "--no-extra", "--no-cpu-baseline",
+                        "--no-matcher", "--no-alone"], capture_output=True, text=True,
+                       timeout=300, env=env)
     assert "torch.distributed.run" in r.stderr and "--nproc-per-node=2" in r.stderr
     if not torch.cuda.is_available():
         assert r.returncode != 0 and r.stdout.strip() == ""

@@ -167,6 +167,13 @@ def test_gpu_error_paths(gpu_ctx):
         gpu_ctx.detect(np.zeros((32, 32)), SiftParams(intervals=0))
     with pytest.raises(RuntimeError, match="parameter"):
         gpu_ctx.detect(np.zeros((32, 32)), SiftParams(window_size=1))
+    # non-finite host doubles: rejected (the extrema scan has no NaN
+    # semantics; include/sift_hip.h input kinds)
+    for bad in (np.nan, np.inf, -np.inf):
+        img = synth_image(64, 48, 1, seed=42)
+        img[10, 20] = bad
+        with pytest.raises(RuntimeError, match="invalid argument"):
+            gpu_ctx.detect(img)
     # the context stays usable after errors
     kps, _ = gpu_ctx.detect(synth_image(64, 48, 1, seed=42))
     assert len(kps) > 0

@@ -63,6 +63,9 @@ struct Bus {
 
 struct Faults {
     bool fail_reserve = false, fail_h2d = false;
+    // word collective number k (0-based over the rank's whole life) fails:
+    // its staging copy (the peers receive the previous words) / its read-back
+    int fail_stage_at = -1, fail_read_at = -1;
 };
 
 struct HostTransport {
@@ -70,13 +73,22 @@ struct HostTransport {
     int r;
     Faults f;
     std::vector<unsigned char> send, recv;
-    int collectives = 0;
+    int collectives = 0, word_calls = 0;
+    int64_t seq = 0;
+    int64_t send_words[8] = {};  // the "device" send buffer of the word collectives
     int rank() const { return r; }
     int nranks() const { return bus->R; }
-    int gather_words(const int64_t* mine, int64_t* all, size_t words) {
+    int64_t next_seq() { return ++seq; }
+    int gather_words(const int64_t* mine, int64_t* all, size_t words, bool* sent) {
         ++collectives;
-        bus->gather(r, mine, all, words * sizeof(int64_t));
-        return SIFT_OK;
+        const int k = word_calls++;
+        *sent = k != f.fail_stage_at;
+        if (*sent) std::memcpy(send_words, mine, words * sizeof(int64_t));
+        std::vector<int64_t> got(words * bus->R);
+        bus->gather(r, send_words, got.data(), words * sizeof(int64_t));
+        if (k == f.fail_read_at) return SIFT_ERR_HIP;
+        std::memcpy(all, got.data(), got.size() * sizeof(int64_t));
+        return *sent ? SIFT_OK : SIFT_ERR_HIP;
     }
     int reserve(size_t slot, unsigned char** ds, unsigned char** dr) {
         if (f.fail_reserve) return SIFT_ERR_NOMEM;
@@ -130,7 +142,10 @@ sift_kp make_rec(int64_t id, size_t k) {
 bool rec_eq(const sift_kp& a, const sift_kp& b) { return std::memcmp(&a, &b, sizeof a) == 0; }
 
 // run one scenario; expect[r] = status rank r must return
-bool scenario(const char* name, const std::vector<RankIn>& in, const std::vector<int>& expect) {
+// (calls > 1: the same transports run the exchange `calls` times, the
+// earlier calls must succeed; statuses and outputs are the last call's)
+bool scenario(const char* name, const std::vector<RankIn>& in, const std::vector<int>& expect,
+              int calls = 1) {
     const int R = (int)in.size();
     Bus bus(R);
     std::vector<int> st(R, 99);
@@ -153,12 +168,17 @@ bool scenario(const char* name, const std::vector<RankIn>& in, const std::vector
             out[r].assign(total_in + 1, sift_kp{});
             oid[r].assign((size_t)R * std::max(1, a.max_local), -7);
             ocnt[r].assign((size_t)R * std::max(1, a.max_local), 7);
-            HostTransport t{&bus, r, a.f, {}, {}, 0};
-            const int n_local = a.bad_arg ? a.max_local + 1 : (int)a.ids.size();
-            st[r] = sift_amd::exchange_records(
-                t, recs.empty() ? nullptr : recs.data(), a.ids.data(), a.counts.data(), n_local,
-                a.max_local, out[r].data(), std::min(a.cap_out, out[r].size()), oid[r].data(),
-                ocnt[r].data(), &nout[r]);
+            HostTransport t{&bus, r, a.f, {}, {}};
+            for (int call = 0; call < calls; ++call) {
+                const bool last = call + 1 == calls;
+                const int n_local = a.bad_arg && last ? a.max_local + 1 : (int)a.ids.size();
+                t.collectives = 0;
+                st[r] = sift_amd::exchange_records(
+                    t, recs.empty() ? nullptr : recs.data(), a.ids.data(), a.counts.data(),
+                    n_local, a.max_local, out[r].data(), std::min(a.cap_out, out[r].size()),
+                    oid[r].data(), ocnt[r].data(), &nout[r]);
+                if (!last && st[r] != SIFT_OK) st[r] = 1000 + st[r];  // an earlier call failed
+            }
             ncoll[r] = t.collectives;
             finished.fetch_add(1);
         });
@@ -250,6 +270,8 @@ int main() {
                    {SIFT_OK, SIFT_OK, SIFT_OK});
     ok &= scenario("world3-all-empty", {rank_of({}, {}, 1), rank_of({}, {}, 1), rank_of({}, {}, 1)},
                    {SIFT_OK, SIFT_OK, SIFT_OK});
+    ok &= scenario("world2-three-calls",
+                   {rank_of({0, 2}, {3, 7}, 2), rank_of({1}, {9}, 2)}, {SIFT_OK, SIFT_OK}, 3);
     ok &= scenario("world4-large",
                    {rank_of({0, 4}, {3000, 10}, 2), rank_of({1, 5}, {1, 2}, 2),
                     rank_of({2}, {777}, 2), rank_of({3, 7}, {0, 5000}, 2)},
@@ -268,6 +290,31 @@ int main() {
         std::vector<RankIn> in = {rank_of({0}, {4}, 1), rank_of({1}, {6}, 1)};
         in[1].bad_arg = true;
         ok &= scenario("world2-badarg-rank1", in, {SIFT_ERR_PEER, SIFT_ERR_ARG});
+    }
+    {  // a rank's header staging fails: the peers see the send buffer's old
+       // words (no valid tag) and count it as failed
+        std::vector<RankIn> in = {rank_of({0}, {4}, 1), rank_of({1}, {6}, 1), rank_of({2}, {2}, 1)};
+        in[1].f.fail_stage_at = 0;
+        ok &= scenario("world3-header-stage-rank1", in,
+                       {SIFT_ERR_PEER, SIFT_ERR_HIP, SIFT_ERR_PEER});
+    }
+    {  // the same in a second call: the stale words are the first call's
+        std::vector<RankIn> in = {rank_of({0}, {4}, 1), rank_of({1}, {6}, 1), rank_of({2}, {2}, 1)};
+        in[2].f.fail_stage_at = 2;
+        ok &= scenario("world3-header-stage-2nd-call", in,
+                       {SIFT_ERR_PEER, SIFT_ERR_PEER, SIFT_ERR_HIP}, 2);
+    }
+    {  // a rank's ready staging fails: the peers see its header words (phase-A tag)
+        std::vector<RankIn> in = {rank_of({0}, {4}, 1), rank_of({1}, {6}, 1)};
+        in[0].f.fail_stage_at = 1;
+        ok &= scenario("world2-ready-stage-rank0", in, {SIFT_ERR_HIP, SIFT_ERR_PEER});
+    }
+    {  // a rank cannot read the headers back: its peers went on to phase B,
+       // where it reports "not ready"
+        std::vector<RankIn> in = {rank_of({0}, {4}, 1), rank_of({1}, {6}, 1), rank_of({2}, {2}, 1)};
+        in[0].f.fail_read_at = 0;
+        ok &= scenario("world3-header-read-rank0", in,
+                       {SIFT_ERR_HIP, SIFT_ERR_PEER, SIFT_ERR_PEER});
     }
     // max_local differs: every rank reports the argument error
     ok &= scenario("world2-maxlocal-mismatch", {rank_of({0}, {4}, 1), rank_of({1}, {6}, 2)},
