@@ -61,11 +61,18 @@ constexpr unsigned kOriWgsAlone = 1024;
 constexpr unsigned kDescWgsAlone = 256u * SIFT_DSPLIT_OCC;  // k_descriptor_split: every resident slot
 constexpr size_t kTileMaxPx = (size_t)1 << 21;    // planes up to this size: LDS-tile blur
 
-// Keypoint lanes: batches alternate between two streams (C, D), each with
+// Keypoint lanes: batches go round-robin over kLanes streams, each lane with
 // its own region of every keypoint array and its own counters, so the chains
 // of consecutive batches run concurrently (within a lane they are serial and
-// the snapshot ranges below stay contiguous).
-constexpr int kLanes = 2;
+// the snapshot ranges below stay contiguous). Two lanes: streams C, D. Four
+// lanes (a job alone; SIFT_LANES=4): C, D, then B once the octaves with a
+// batch of their own have their tail levels there, and A for the final
+// batch right behind the small octaves, so no chain waits for another.
+#ifndef SIFT_LANES
+#define SIFT_LANES 2
+#endif
+constexpr int kLanes = SIFT_LANES;
+static_assert(kLanes == 2 || kLanes == 4, "keypoint lanes: 2 or 4");
 constexpr int kSlots = SIFT_MAX_INFLIGHT;
 constexpr int kPairs = 2;
 // device counter block of a slot: [4L..4L+3] live counters of lane L
@@ -720,7 +727,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         return st;
 
     const int lanes = s.lanes;
-    hipStream_t lane_stream[kLanes] = {sC, sD};
+    hipStream_t lane_stream[4] = {sC, sD, sB, sA};
     SIFT_HIP_TRY(launch_job_begin(&s.d_stage->pt, s.h_pt.jp, s.d_ctr, kCtrWords, sA));
 
     auto blur = [&](hipStream_t so, int o, int l, const double* bsrc, size_t src_bs,
@@ -842,11 +849,24 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
         return SIFT_OK;
     };
     int n_batches = 0;
-    // batch gb (lane gb % lanes): octaves [o_begin, o_end), whose levels
-    // were enqueued on `sps`
+    int lane_last[4] = {-1, -1, -1, -1};  // the lane's previous batch
+    int lane_rr = 0;
+    // batch gb: octaves [o_begin, o_end), whose levels were enqueued on
+    // `sps`. Lanes round-robin; with four lanes the per-octave batches take
+    // lanes 0-2 (C, D, B) and the final batch lane 3 (A, free once the
+    // pyramid is done), so no per-octave chain delays the pyramid on A.
     auto batch = [&](int o_begin, int o_end, std::initializer_list<hipStream_t> sps) -> int {
         const int gb = n_batches++;
-        const int L = gb % lanes;
+        const bool final_batch = o_end == g.octaves;
+        int L;
+        if (lanes > 2 && final_batch) {
+            L = 3;
+        } else {
+            L = lane_rr % (lanes > 2 ? 3 : lanes);
+            ++lane_rr;
+        }
+        const int prev = lane_last[L];
+        lane_last[L] = gb;
         const hipStream_t sx = lane_stream[L];
         for (hipStream_t sp : sps) {
             if (sp == sx) continue;  // same stream: already ordered
@@ -855,7 +875,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             SIFT_HIP_TRY(hipEventRecord(pyr_done, sp));
             SIFT_HIP_TRY(hipStreamWaitEvent(sx, pyr_done, 0));
         }
-        return run_chain(L, o_begin, o_end, gb < lanes ? zeros : snap(gb - lanes), snap(gb), sx);
+        return run_chain(L, o_begin, o_end, prev < 0 ? zeros : snap(prev), snap(gb), sx);
     };
     // Two pyramid streams (a job alone): the decimation chain on A — levels
     // 1 .. intervals of every octave, octave o+1 needs only level
@@ -866,9 +886,12 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // and every octave switch paid a cross-stream join on the chain).
     // One stream (a pipelined job): in order.
     const bool two_pyr = sA != sB;
+    // with four lanes the batch of octave 2 runs on B: the tail levels of the
+    // octaves of the final batch then go on A, so they never queue behind it
+    const int o_tail_end = kLanes > 2 ? o_merge : o_small;
     for (int o = 0; o < o_small; ++o) {
         for (int l = 1; l < g.n_gauss; ++l) {
-            const bool tail = two_pyr && l > dec_level;
+            const bool tail = two_pyr && l > dec_level && o < o_tail_end;
             hipStream_t so = tail ? sB : sA;
             if (tail && l == dec_level + 1) {
                 hipEvent_t chain_ev = sync_event(s);
@@ -905,15 +928,24 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     }
     // (the final batch of a job alone on stream A right behind k_octaves_lds,
     // saving the lane stream's wait: synchronous latency +1.2 %, r05_s)
-    if (o_merge < g.octaves && (st = batch(o_merge, g.octaves, {sA, sB})) != SIFT_OK) return st;
-    // lane D joins C for the age counter (k_job_done): the job's last device
-    // work. The host does not wait for it: each lane's last descriptor launch
-    // publishes the lane's counters with its record range (ExportSink), so
-    // the job is complete on the host once its chains' events are.
-    if (sD != sC) {
+    // (four lanes: the final batch's octaves were built on A alone; B holds
+    // the octave-2 chain, which it must not wait for)
+    if (o_merge < g.octaves &&
+        (st = (kLanes > 2 && two_pyr) ? batch(o_merge, g.octaves, {sA})
+                                      : batch(o_merge, g.octaves, {sA, sB})) !=
+            SIFT_OK)
+        return st;
+    // the other lane streams join C for the age counter (k_job_done): the
+    // job's last device work. The host does not wait for it: each lane's last
+    // descriptor launch publishes the lane's counters with its record range
+    // (ExportSink), so the job is complete on the host once its chains' events
+    // are.
+    for (hipStream_t sj : {sD, sB, sA}) {
+        if (sj == sC || (kLanes == 2 && sj != sD)) continue;
+        if (sj == sB && sB == sD) continue;
         hipEvent_t jd = sync_event(s);
         if (!jd) return SIFT_ERR_HIP;
-        SIFT_HIP_TRY(hipEventRecord(jd, sD));
+        SIFT_HIP_TRY(hipEventRecord(jd, sj));
         SIFT_HIP_TRY(hipStreamWaitEvent(sC, jd, 0));
     }
     if (s.taps_init.jp.done) {

@@ -16,7 +16,16 @@
 #define SIFT_DESC_AHEAD 1
 #endif
 #ifndef SIFT_DESC_SWZ  // replica swizzle of the histogram bins (hist_slot)
-#define SIFT_DESC_SWZ 2
+#define SIFT_DESC_SWZ 0
+#endif
+#ifndef SIFT_DESC_PERM  // 1: lanes sharing a replica take samples 16 apart (sample_of_lane)
+#define SIFT_DESC_PERM 0
+#endif
+#ifndef SIFT_DESC_BSTRIDE  // doubles between consecutive bins of a replica (>= replicas)
+#define SIFT_DESC_BSTRIDE SIFT_DSPLIT_REPS
+#endif
+#ifndef SIFT_DESC_RMAJOR  // > 0: replica-major layout, replicas SIFT_DESC_RMAJOR + 128 doubles apart
+#define SIFT_DESC_RMAJOR 0
 #endif
 
 namespace sift_amd {
@@ -83,13 +92,17 @@ __device__ __forceinline__ DescRecord load_record(const PyrTable* pt, const DevP
 // neighbouring cells to other banks. It only relocates the slot: the adds
 // into a given (replica, bin) and their order are unchanged, so every
 // histogram is bit-identical.
+constexpr int kBinStride = SIFT_DESC_BSTRIDE;
+static_assert(kBinStride >= SIFT_DSPLIT_REPS, "bin stride");
+
 template <int NR>
 __device__ __forceinline__ int hist_slot(int i, int r) {
     int f = 0;
     if (SIFT_DESC_SWZ == 1) f = i >> 2;                                // ori bit 2, col_bin
     if (SIFT_DESC_SWZ == 2) f = ((i >> 3) & 3) | (((i >> 5) & 1) << 2);  // col_bin, row_bin bit 0
     if (SIFT_DESC_SWZ == 3) f = i >> 1;
-    return i * NR + (r ^ (f & (NR - 1)));
+    if (SIFT_DESC_RMAJOR > 0) return (r ^ (f & (NR - 1))) * (128 + SIFT_DESC_RMAJOR) + i;
+    return i * kBinStride + (r ^ (f & (NR - 1)));
 }
 
 // ---------------------------------------------------------------------------
@@ -170,10 +183,22 @@ __device__ __forceinline__ void add_sample_f64(double* hist, int r, int scol, in
 //    unconditionally: lanes past the end read pixel (1, 1), so the compiler
 //    can count them).
 // ---------------------------------------------------------------------------
+// Sample t0 + sample_of_lane(lane) of a step goes to lane `lane`. With
+// SIFT_DESC_PERM the lanes that share a replica (lane & 7) within an LDS
+// lane group take samples 16 apart instead of 8 (lane r + 8h + 32G <- sample
+// r + 8G + 16h): the samples of one replica still go to the same replica
+// (sample & 7 == lane & 7), but neighbouring samples, which mostly hit the
+// same bin, no longer meet on one address inside one atomic instruction.
+__device__ __forceinline__ int sample_of_lane(int lane) {
+    if (!SIFT_DESC_PERM) return lane;
+    return (lane & 7) | ((lane >> 5) << 3) | (((lane >> 3) & 3) << 4);
+}
+
 template <int NR>
 __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, double* hist,
                                           const double2* atab, const double* gtab) {
     const int lane = threadIdx.x & 63;
+    const int slane = sample_of_lane(lane);
     const int side = 2 * d.radius + 1;
     gdouble* img = gbl(d.img);
     const int W = d.W, H = d.H, x = d.x, y = d.y, radius = d.radius;
@@ -212,7 +237,7 @@ __device__ __forceinline__ void desc_walk(const DescRecord& d, int j0, int dj, d
         }
         const int total = __builtin_amdgcn_readlane(pre, 63);
         auto locate = [&](int t0, int& srow, int& scol) -> bool {
-            const int t = t0 + lane;
+            const int t = t0 + slane;
             int r = 0;
 #pragma unroll
             for (int step = 32; step >= 1; step >>= 1)
@@ -338,6 +363,9 @@ constexpr int kSplitReps = SIFT_DSPLIT_REPS;
 // Gaussian weight table G(0..radius) of the current record: one exp per thread per record instead of one per sample; records
 // with a larger radius evaluate exp per sample
 constexpr int kGTab = 256;
+// one wave's replicas: 128 bins (the last one padded to a full stride), even
+constexpr int kHistWave = SIFT_DESC_RMAJOR > 0 ? (SIFT_DSPLIT_REPS * (128 + SIFT_DESC_RMAJOR) + 1) & ~1
+                                               : (128 * kBinStride + 1) & ~1;
 static_assert(kSplitReps >= 1 && kSplitReps <= 16 && (kSplitReps & (kSplitReps - 1)) == 0,
               "replicas: a power of two <= 16");
 
@@ -346,7 +374,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     const RecSide* __restrict__ rec_side, const unsigned* __restrict__ rec_begin,
     const unsigned* __restrict__ n_rec, unsigned cap_rec, float* __restrict__ desc_f32,
     unsigned* __restrict__ work, ExportSink ex) {
-    __shared__ __attribute__((aligned(16))) double hist_all[4 * 128 * kSplitReps];
+    __shared__ __attribute__((aligned(16))) double hist_all[4 * kHistWave];
     __shared__ double2 atab[17];
     __shared__ unsigned next_k;
     __shared__ double2 next_sc;  // sin, cos of the next record's pori
@@ -354,7 +382,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
     set_job_prio(pt->jp, 0);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double* const hist = hist_all + wv * 128 * kSplitReps;
+    double* const hist = hist_all + wv * kHistWave;
     const unsigned n = min(*n_rec, cap_rec);
     const unsigned k0 = min(*rec_begin, n);
     // the launch's record range is fixed before it starts (orientation has
@@ -391,7 +419,7 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
             const double i = (double)threadIdx.x;
             gtab[threadIdx.x] = exp_f64(-(i * i) / (0.5 * kDescW * kDescW * d.hw * d.hw));
         }
-        for (int i = lane; i < 64 * kSplitReps; i += 64)
+        for (int i = lane; i < kHistWave / 2; i += 64)
             reinterpret_cast<double2*>(hist)[i] = make_double2(0.0, 0.0);
         __syncthreads();  // the table (uniform: every thread gets here)
         desc_walk<kSplitReps>(d, wv, 4, hist, atab, use_tab ? gtab : nullptr);
@@ -405,8 +433,8 @@ __global__ __launch_bounds__(256, SIFT_DSPLIT_OCC) void k_descriptor_split(
         if (wv == 0) {
 #pragma unroll
             for (int w = 1; w < 4; ++w) {  // the partials in wave order
-                v0 += hist_all[w * 128 * kSplitReps + lane];
-                v1 += hist_all[w * 128 * kSplitReps + lane + 64];
+                v0 += hist_all[w * kHistWave + lane];
+                v1 += hist_all[w * kHistWave + lane + 64];
             }
             finish_record(v0, v1, d, k, recs, desc_f32, ex);
         } else if (wv == 1 && lane == 0) {

@@ -65,6 +65,26 @@
 #ifndef SIFT_BLUR_PAIR_ROWS  // k_blur_pair: output rows per wave (a pair: twice that)
 #define SIFT_BLUR_PAIR_ROWS 32
 #endif
+// k_blur_pair source rows: staged by LDS-DMA into a ring of this many lines
+// per wave (k_blur_pair_dma), or 0: through registers (k_blur_pair) — on
+// planes of at least 2^SIFT_BLUR_DMA_PX_LOG2 pixels and radii up to
+// SIFT_BLUR_DMA_MAXR. Measured (tools/blur_lab.hip, r06_s1 / r06_s2, every
+// plane bit-identical): 4096^2 R = 5 / 7 / 10 -4.8 / -13.8 / -3.8 %, 8192^2
+// R = 5 / 7 -5.6 / -11.1 % but R = 10 +5.4 %, 15360x8640 R = 4..8 -3.6..-5.3 %
+// but R = 10 +2.9 %, 3840x2160 (1080p's octave 0) +2.7..+6 %; ring depth 2 or
+// 8 no better than 4. In the pipelined big-config legs the kernel's larger
+// LDS footprint (52 KB per workgroup at R = 8) costs more than it saves:
+// config 5 10.01 vs 9.66 ms per image, config 3 3.63 vs 3.65 (r06_s3), so the
+// default is off; the kernel stays as the measured alternative.
+#ifndef SIFT_BLUR_DMA
+#define SIFT_BLUR_DMA 0
+#endif
+#ifndef SIFT_BLUR_DMA_MAXR
+#define SIFT_BLUR_DMA_MAXR 8
+#endif
+#ifndef SIFT_BLUR_DMA_PX_LOG2
+#define SIFT_BLUR_DMA_PX_LOG2 24
+#endif
 #ifndef SIFT_ORI_AHEAD  // k_orient_wave: steps of 64 samples whose loads are in flight
 #define SIFT_ORI_AHEAD 1
 #endif
@@ -540,6 +560,192 @@ __global__ __launch_bounds__(256) void k_blur_pair(const double* __restrict__ sr
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_blur_pair_dma<R, C, DECIM, NB>: k_blur_pair with its source rows staged
+// by LDS-DMA (global_load_lds_dword: the loads write LDS directly, no VGPR
+// destination). Each wave owns a ring of NB row lines; the row of walk step
+// s + NB - 1 is issued into the line step s - 1 consumed, so NB - 1 rows are
+// in flight while step s runs, at no VGPR cost (k_blur_pair holds its PF = 2
+// rows in flight in registers, 12 VGPRs at C = 2, and stages each through a
+// ds_write). A line holds source columns x0 - R .. x0 - R + LW - 1, clamped
+// per double (replicate border) — each lane moves one 4-B half of a double,
+// so the clamp is exact at both borders. The wait for step s's row is a
+// counted vmcnt over the DMA instructions issued after it (loads complete in
+// order; the column pass's stores only make the wait stricter). Same walk,
+// same per-output arithmetic and order as k_blur_pair: bit-identical planes.
+// LDS (dynamic): ring [4 waves][NB][LW] + hand-over [4][R][64 C] doubles.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One global_load_lds_dword: this lane's 4 bytes at `g` land at LDS address
+// lds + 4 * lane. Issued as inline asm, so the compiler's wait insertion does
+// not see an LDS write in flight (it would put vmcnt(0) before every LDS
+// read); the kernels wait with counted vm_wait<N> instead.
+__device__ __forceinline__ void dma_dword(const void* g, const double* lds) {
+    // M0 (the DMA's LDS base) is compiler-reserved: saved and restored in the
+    // same statement; s_nop 0 covers the M0 write -> LDS-DMA hazard
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)lds);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(m0)
+        : "memory");
+}
+
+template <int R, int C>
+constexpr int pair_dma_lw() {  // line width in doubles: 32-double DMA pieces
+    return (64 * C + 2 * R + 31) / 32 * 32;
+}
+template <int R, int C, int NB>
+constexpr size_t pair_dma_lds_bytes() {
+    return ((size_t)4 * NB * pair_dma_lw<R, C>() + (size_t)4 * R * 64 * C) * sizeof(double);
+}
+
+template <int R, int C, bool DECIM, int NB>
+__global__ __launch_bounds__(256) void k_blur_pair_dma(const double* __restrict__ src,
+                                                       size_t src_bs, double* __restrict__ dst,
+                                                       size_t bs, int W, int H, int rows,
+                                                       BlurTaps taps, double* __restrict__ dec,
+                                                       int Wd, int Hd) {
+    set_job_prio(taps.jp, SIFT_PRIO_STRIP);
+    constexpr int NW = 2 * R + 2;
+    constexpr int SPAN = 64 * C;
+    constexpr int LW = pair_dma_lw<R, C>();
+    constexpr int NI = LW / 32;  // 4-B DMA instructions per row
+    static_assert((NB & (NB - 1)) == 0 && NB >= 2, "ring depth: a power of two");
+    static_assert(NI * (NB - 1) <= 63, "vmcnt range");
+    extern __shared__ __attribute__((aligned(16))) double lds_pair[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool down = (wv & 1) != 0;
+    int bx, by, bz;
+    xcd_remap(bx, by, bz);
+    if (by * 4 * rows >= H) return;  // the whole workgroup lies below the image
+    src += bz * src_bs;
+    dst += bz * bs;
+    if (DECIM) dec += bz * bs;
+    const int x0 = bx * SPAN;
+    const int b = (2 * (by * 2 + (wv >> 1)) + 1) * rows;  // the pair's boundary row
+    double* const ring = lds_pair + wv * NB * LW;
+    double* const xch = lds_pair + 4 * NB * LW;  // [4][R][SPAN]
+    // byte offset, within a source row, of this lane's 4-B piece of DMA
+    // instruction q: line double 32 q + lane / 2, half lane & 1
+    unsigned gofs[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q)
+        gofs[q] = (unsigned)clampi(x0 - R + 32 * q + (lane >> 1), 0, W - 1) * 8u + 4u * (lane & 1);
+    double k[R + 1];
+#pragma unroll
+    for (int u = 0; u <= R; ++u) k[u] = taps.k[u];
+    const double sw = taps.sum_w, inv = taps.inv;
+    const int last = R + rows;  // walk steps s = 0 .. last stage position R + s
+    auto issue = [&](int s) {   // the row of step s (clamped to the last) into its line
+        const int p = R + min(s, last);
+        const int ry = clampi(down ? b - R + p : b - 1 + R - p, 0, H - 1);
+        const char* rp = reinterpret_cast<const char*>(src + (size_t)ry * W);
+        double* const line = ring + (s & (NB - 1)) * LW;
+        asm volatile("" ::: "memory");  // after the previous reads of that line
+#pragma unroll
+        for (int q = 0; q < NI; ++q) dma_dword(rp + gofs[q], line + 32 * q);
+    };
+    auto row_pass = [&](int s, double* hn) {  // of the row of step s
+        const double* const sl = ring + (s & (NB - 1)) * LW;
+        double v[C + 2 * R];
+        if (C == 2) {
+            const double2* s2 = reinterpret_cast<const double2*>(sl + 2 * lane);
+#pragma unroll
+            for (int q = 0; q < (C + 2 * R) / 2; ++q) {
+                const double2 t = s2[q];
+                v[2 * q] = t.x;
+                v[2 * q + 1] = t.y;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < C + 2 * R; ++q) v[q] = sl[lane + q];
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            double acc = v[c + R] * k[0];
+#pragma unroll
+            for (int u = 1; u <= R; ++u) acc += k[u] * (v[c + R + u] + v[c + R - u]);
+            hn[c] = div_sum_w(acc, sw, inv);
+        }
+    };
+#pragma unroll
+    for (int s = 0; s + 1 < NB; ++s) issue(s);
+    double win[C][NW];
+    // prologue: own positions R .. 2R-1 (steps 0 .. R-1), also handed to the partner
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        issue(j + NB - 1);
+        vm_wait<(NB - 1) * NI>();
+        double hn[C];
+        row_pass(j, hn);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            win[c][R + j] = hn[c];
+            xch[(wv * R + j) * SPAN + C * lane + c] = hn[c];
+        }
+    }
+    // workgroup barrier that leaves the DMAs in flight (__syncthreads would
+    // drain them: vmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int c = 0; c < C; ++c) win[c][R - 1 - j] = xch[((wv ^ 1) * R + j) * SPAN + C * lane + c];
+    if (down ? b >= H : b - rows >= H) {  // no output row of this wave in the image
+        vm_wait<0>();
+        return;
+    }
+    const int xa = x0 + C * lane;
+    for (int kb = 0; kb <= rows; kb += NW) {
+#pragma unroll
+        for (int t = 0; t < NW; ++t) {
+            const int kk = kb + t;
+            if (kk <= rows) {
+                const int s = R + kk;
+                issue(s + NB - 1);
+                vm_wait<(NB - 1) * NI>();
+                double hn[C];
+                row_pass(s, hn);
+                if (kk >= 1) {
+                    const int y = down ? b + kk - 1 : b - kk;
+                    double o[C];
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        double a = win[c][(t + R - 1 + NW) % NW] * k[0];
+#pragma unroll
+                        for (int u = 1; u <= R; ++u)
+                            a += k[u] * (win[c][(t + R - 1 + u) % NW] +
+                                         win[c][(t + R - 1 - u + 2 * NW) % NW]);
+                        o[c] = div_sum_w(a, sw, inv);
+                    }
+                    if (y < H && xa < W) {
+                        if (C == 2)  // W is even for C == 2 (launcher)
+                            *reinterpret_cast<double2*>(dst + (size_t)y * W + xa) =
+                                make_double2(o[0], o[C - 1]);
+                        else
+                            dst[(size_t)y * W + xa] = o[0];
+                        if (DECIM && !(y & 1) && (y >> 1) < Hd && (C == 2 || !(xa & 1)) &&
+                            (xa >> 1) < Wd)
+                            dec[(size_t)(y >> 1) * Wd + (xa >> 1)] = o[0];
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < C; ++c) win[c][(2 * R + t) % NW] = hn[c];
+            }
+        }
+    }
+    vm_wait<0>();  // the ring's last (unused) rows land before the wave ends
 }
 
 // ---------------------------------------------------------------------------
@@ -1527,11 +1733,45 @@ static hipError_t launch_blur_r(const BlurSource& src, double* dst, size_t bs, i
                         W, H, rows, taps, dec, Wd, Hd);
 }
 
+template <int R, int C, int NB>
+static hipError_t launch_pair_dma_r(const double* src, size_t src_bs, double* dst, size_t bs,
+                                    int n_img, int W, int H, int rows, const BlurTaps& taps,
+                                    double* dec, int Wd, int Hd, hipStream_t s, hipEvent_t e0,
+                                    hipEvent_t e1) {
+    const dim3 grid((W + 64 * C - 1) / (64 * C), (H + 4 * rows - 1) / (4 * rows), n_img);
+    constexpr size_t lds = pair_dma_lds_bytes<R, C, NB>();
+    static_assert(lds <= 160 * 1024, "k_blur_pair_dma: LDS");
+    static bool attr = false;  // above 64 KB of dynamic LDS (benign race: idempotent)
+    if (!attr) {
+        const hipError_t e = (lds > 64 * 1024)
+            ? hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blur_pair_dma<R, C, true, NB>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)
+            : hipSuccess;
+        const hipError_t e2 = (lds > 64 * 1024)
+            ? hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blur_pair_dma<R, C, false, NB>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)
+            : hipSuccess;
+        if (e != hipSuccess) return e;
+        if (e2 != hipSuccess) return e2;
+        attr = true;
+    }
+    if (dec)
+        return launch_timed(k_blur_pair_dma<R, C, true, NB>, grid, dim3(256), lds, s, e0, e1, src,
+                            src_bs, dst, bs, W, H, rows, taps, dec, Wd, Hd);
+    return launch_timed(k_blur_pair_dma<R, C, false, NB>, grid, dim3(256), lds, s, e0, e1, src,
+                        src_bs, dst, bs, W, H, rows, taps, dec, Wd, Hd);
+}
+
 template <int R, int C>
 static hipError_t launch_pair_r(const double* src, size_t src_bs, double* dst, size_t bs,
                                 int n_img, int W, int H, int rows, const BlurTaps& taps,
                                 double* dec, int Wd, int Hd, hipStream_t s, hipEvent_t e0,
                                 hipEvent_t e1) {
+    if constexpr (SIFT_BLUR_DMA > 0 && R <= SIFT_BLUR_DMA_MAXR) {
+        if ((size_t)W * H >= ((size_t)1 << SIFT_BLUR_DMA_PX_LOG2))
+            return launch_pair_dma_r<R, C, (SIFT_BLUR_DMA > 0 ? SIFT_BLUR_DMA : 2)>(
+                src, src_bs, dst, bs, n_img, W, H, rows, taps, dec, Wd, Hd, s, e0, e1);
+    }
     const dim3 grid((W + 64 * C - 1) / (64 * C), (H + 4 * rows - 1) / (4 * rows), n_img);
     if (dec)
         return launch_timed(k_blur_pair<R, C, true>, grid, dim3(256), 0, s, e0, e1, src, src_bs,

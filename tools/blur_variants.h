@@ -354,6 +354,23 @@ hipError_t launch_pair_lab(const double* src, double* dst, int W, int H, int row
 using VarFn = hipError_t (*)(const double*, double*, int, int, int, const BlurTaps&, double*, int,
                              int, hipStream_t, hipEvent_t, hipEvent_t);
 
+// k_blur_pair_dma (the library's LDS-DMA pair walk) at an explicit shape and
+// ring depth NB (env LAB_NB: 2, 4 or 8; default 4)
+template <int R, int C, int NB>
+hipError_t launch_pdma_lab(const double* src, double* dst, int W, int H, int rows,
+                           const BlurTaps& t, double* dec, int Wd, int Hd, hipStream_t s,
+                           hipEvent_t e0, hipEvent_t e1) {
+    return launch_pair_dma_r<R, C, NB>(src, 0, dst, 0, 1, W, H, rows, t, dec, Wd, Hd, s, e0, e1);
+}
+template <int R, int C>
+VarFn pick_pdma() {
+    const char* e = std::getenv("LAB_NB");
+    const int nb = e ? std::atoi(e) : 4;
+    if (nb == 2) return &launch_pdma_lab<R, C, 2>;
+    if (nb == 8) return &launch_pdma_lab<R, C, 8>;
+    return &launch_pdma_lab<R, C, 4>;
+}
+
 // radii the lab instantiates (octave-0 levels of intervals 3 and 2)
 #define LAB_RADII(X) X(4) X(5) X(6) X(7) X(8) X(10) X(14)
 
@@ -364,6 +381,8 @@ inline VarFn pick(const char* kind, int C, int R) {
         if (!std::strcmp(kind, "ud")) return C == 2 ? &launch_ud_r<RR, 2> : &launch_ud_r<RR, 1>; \
         if (!std::strcmp(kind, "pair"))                                                \
             return C == 2 ? &launch_pair_lab<RR, 2> : &launch_pair_lab<RR, 1>;        \
+        if (!std::strcmp(kind, "pdma"))                                                \
+            return C == 2 ? pick_pdma<RR, 2>() : pick_pdma<RR, 1>();                   \
         if (!std::strcmp(kind, "strip"))                                               \
             return C == 2 ? &launch_strip_r<RR, 2> : &launch_strip_r<RR, 1>;          \
     }
