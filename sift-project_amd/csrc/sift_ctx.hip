@@ -69,7 +69,7 @@ constexpr size_t kTileMaxPx = (size_t)1 << 21;    // planes up to this size: LDS
 // batch of their own have their tail levels there, and A for the final
 // batch right behind the small octaves, so no chain waits for another.
 #ifndef SIFT_LANES
-#define SIFT_LANES 2
+#define SIFT_LANES 4
 #endif
 constexpr int kLanes = SIFT_LANES;
 static_assert(kLanes == 2 || kLanes == 4, "keypoint lanes: 2 or 4");
@@ -214,6 +214,7 @@ struct Slot {
     Mapped<sift_kp> exp_rec;
     Mapped<RecSide> exp_side;
     Mapped<unsigned> exp_cnt;  // [begin, end) per chain
+    DevBuf<unsigned> flow_ctr;  // k_octaves_flow ticket / error / band counters
     size_t exp_lane = 0;
     std::vector<hipEvent_t> chain_ev, sync_ev, ev_pool;
     std::vector<int> chain_lane;
@@ -297,6 +298,18 @@ struct sift_ctx {
     // which then takes 76 instead of 47 us; synchronous latency)
     size_t lds_max_px = kLdsOctaveMaxPx;
     size_t lds_max_px_shared = kLdsOctavePx;
+    // octaves of the final batch up to this many pixels per image, above the
+    // LDS octaves, in flight in one k_octaves_flow launch of flow_wgs
+    // workgroups (SIFT_FLOW=1; SIFT_FLOW_PX, SIFT_FLOW_WGS). Off by default:
+    // bit-exact, but a tile's dependent latency (~5 us: sc1 staging, two LDS
+    // passes at one wave per SIMD, write-through drain, counter hand-off) is
+    // no shorter than a dependent launch, and levels depend on levels.
+    // Measured (r06_s6/s7): 1080p octaves 3-5 80 vs 78.5 us back to back,
+    // octaves 2-5 alone 137.6 vs 99 us, synchronous latency 0.769 vs 0.753
+    // ms, the driver's command 0.560 vs 0.539 ms per step.
+    bool flow = false;
+    size_t flow_max_px = (size_t)1 << 19;
+    int flow_wgs = 128;
     bool serial = false;  // SIFT_SERIAL=1: every kernel on one stream (profiling)
     // Kernels raise their waves' issue priority by their job's age rank
     // (JobPrio; -1.3 % on the driver's bench command, round 3); d_done
@@ -728,7 +741,76 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
 
     const int lanes = s.lanes;
     hipStream_t lane_stream[4] = {sC, sD, sB, sA};
-    SIFT_HIP_TRY(launch_job_begin(&s.d_stage->pt, s.h_pt.jp, s.d_ctr, kCtrWords, sA));
+    const int dec_level = g.n_gauss - 3;  // = intervals (sift.cpp:195-196)
+    // octaves from o_small on are small enough to run LDS-resident in one
+    // launch (k_octaves_lds); the larger ones get one k_blur launch per level
+    int o_small = g.octaves;
+    const size_t lds_px = (s.lanes == 1 && n_img == 1 && !ctx->serial) ? ctx->lds_max_px_shared
+                                                                        : ctx->lds_max_px;
+    for (int o = 0; o < g.octaves; ++o)
+        if (lds_octave_fits(g.W[o], g.H[o]) && (size_t)(g.W[o] | 1) * g.H[o] <= lds_px) {
+            o_small = o;
+            break;
+        }
+    // Keypoint batches: each large octave (>= batch_px pixels over the job's
+    // images) is its own batch as soon as its levels exist; the smaller ones,
+    // whose keypoint work is too small to amortise a chain of launches, form
+    // one final batch. The final batch starts no later than o_small: octaves
+    // built by k_octaves_lds have no per-octave batch of their own.
+    const size_t batch_px = (size_t)1 << ((s.lanes > 1 || n_img > 1) ? ctx->batch_px_log2_alone
+                                                                  : ctx->batch_px_log2);
+    int o_merge = g.octaves;  // first octave of the final batch
+    for (int o = 0; o < g.octaves; ++o)
+        if ((size_t)g.W[o] * g.H[o] * n_img < batch_px) {
+            o_merge = o;
+            break;
+        }
+    o_merge = std::min(o_merge, o_small);
+    // octaves [o_flow, o_small): in flight in one k_octaves_flow launch (the
+    // final batch's octaves above the LDS ones, at most flow_max_px pixels)
+    int o_flow = o_small;
+    FlowGrid fg;
+    std::memset(&fg, 0, sizeof fg);
+    int flow_words = 0;
+    if (ctx->flow) {
+        for (int o = o_merge; o < o_small; ++o)
+            if ((size_t)g.W[o] * g.H[o] <= ctx->flow_max_px) {
+                o_flow = o;
+                break;
+            }
+        bool ok = o_flow < o_small && (o_small - o_flow) * (g.n_gauss - 1) <= kFlowMaxGroups;
+        for (int l = 1; ok && l < g.n_gauss; ++l) ok = s.taps[l].R >= 1 && s.taps[l].R <= kFlowMaxR;
+        if (ok) {
+            fg.n_img = n_img;
+            fg.err = 1;
+            flow_words = 2;  // ticket, error flag
+            for (int o = o_flow; o < o_small; ++o)
+                for (int l = 1; l < g.n_gauss; ++l) {
+                    FlowGroup& G = fg.g[fg.n_groups];
+                    G.o = o;
+                    G.l = l;
+                    G.W = g.W[o];
+                    G.H = g.H[o];
+                    G.nbx = (G.W + 63) / 64;
+                    G.nby = (G.H + 31) / 32;
+                    G.first = fg.total;
+                    fg.total += G.nby * n_img * G.nbx;
+                    G.cnt = flow_words;
+                    flow_words += n_img * G.nby;
+                    G.dep = l >= 2 ? fg.n_groups - 1
+                                   : (o > o_flow ? (o - 1 - o_flow) * (g.n_gauss - 1) + dec_level - 1
+                                                 : -1);
+                    G.dep_dec = l == 1 && o > o_flow;
+                    G.dec = l == dec_level && o + 1 < g.octaves;
+                    ++fg.n_groups;
+                }
+            if ((st = s.flow_ctr.ensure(flow_words)) != SIFT_OK) return st;
+        } else {
+            o_flow = o_small;
+        }
+    }
+    SIFT_HIP_TRY(launch_job_begin(&s.d_stage->pt, s.h_pt.jp, s.d_ctr, kCtrWords,
+                                  flow_words ? s.flow_ctr.p : nullptr, flow_words, sA));
 
     auto blur = [&](hipStream_t so, int o, int l, const double* bsrc, size_t src_bs,
                     const BlurTaps& t, bool dec) -> int {
@@ -789,31 +871,6 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 return st;
         }
     }
-    const int dec_level = g.n_gauss - 3;  // = intervals (sift.cpp:195-196)
-    // octaves from o_small on are small enough to run LDS-resident in one
-    // launch (k_octaves_lds); the larger ones get one k_blur launch per level
-    int o_small = g.octaves;
-    const size_t lds_px = (s.lanes == 1 && n_img == 1 && !ctx->serial) ? ctx->lds_max_px_shared
-                                                                        : ctx->lds_max_px;
-    for (int o = 0; o < g.octaves; ++o)
-        if (lds_octave_fits(g.W[o], g.H[o]) && (size_t)(g.W[o] | 1) * g.H[o] <= lds_px) {
-            o_small = o;
-            break;
-        }
-    // Keypoint batches: each large octave (>= batch_px pixels over the job's
-    // images) is its own batch as soon as its levels exist; the smaller ones,
-    // whose keypoint work is too small to amortise a chain of launches, form
-    // one final batch. The final batch starts no later than o_small: octaves
-    // built by k_octaves_lds have no per-octave batch of their own.
-    const size_t batch_px = (size_t)1 << ((s.lanes > 1 || n_img > 1) ? ctx->batch_px_log2_alone
-                                                                  : ctx->batch_px_log2);
-    int o_merge = g.octaves;  // first octave of the final batch
-    for (int o = 0; o < g.octaves; ++o)
-        if ((size_t)g.W[o] * g.H[o] * n_img < batch_px) {
-            o_merge = o;
-            break;
-        }
-    o_merge = std::min(o_merge, o_small);
     const unsigned* zeros = s.d_ctr + kCtrZeros;
     auto snap = [&](int gb) { return s.d_ctr + kCtrSnap + 4 * gb; };
     // records of every chain also go to the mapped export buffers, sized from
@@ -890,7 +947,20 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // octaves of the final batch then go on A, so they never queue behind it
     const int o_tail_end = kLanes > 2 ? o_merge : o_small;
     for (int o = 0; o < o_small; ++o) {
-        for (int l = 1; l < g.n_gauss; ++l) {
+        if (o == o_flow) {  // octaves [o_flow, o_small) on A, one launch
+            double bytes = 0.0;
+            for (int q = o_flow; q < o_small; ++q) {
+                bytes += 16.0 * (g.n_gauss - 1) * (double)g.W[q] * (double)g.H[q];
+                if (q + 1 < g.octaves) bytes += 8.0 * (double)g.W[q + 1] * (double)g.H[q + 1];
+            }
+            hipEvent_t e0, e1;
+            if (prof_events(ctx, s, &e0, &e1, bytes * n_img, SIFT_PROF_PYRAMID + o_flow) !=
+                SIFT_OK)
+                return SIFT_ERR_HIP;
+            SIFT_HIP_TRY(launch_octaves_flow(d_pt, fg, s.d_stage->taps, s.flow_ctr.p,
+                                             ctx->flow_wgs, sA, e0, e1));
+        }
+        for (int l = 1; o < o_flow && l < g.n_gauss; ++l) {
             const bool tail = two_pyr && l > dec_level && o < o_tail_end;
             hipStream_t so = tail ? sB : sA;
             if (tail && l == dec_level + 1) {
@@ -904,7 +974,7 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
                 return st;
         }
         if (o == 0 && ctx->pyr_chain) {
-            SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, two_pyr ? sB : sA));
+            SIFT_HIP_TRY(hipEventRecord(s.pyr0_ev, two_pyr && o < o_flow ? sB : sA));
             ctx->pyr_last = (int)(&s - ctx->slots);
         }
         // two pyramid streams: B joined A before the octave's tail levels, so
@@ -1068,7 +1138,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     }
     if (s.exported && s.n_keys != n_ori) s.exported = false;
     ctx->exp_px_hint = std::max(ctx->exp_px_hint,
-                                (double)std::max(s.n_lane[0], s.n_lane[1]) /
+                                (double)*std::max_element(s.n_lane, s.n_lane + kLanes) /
                                     ((double)g.W[0] * (double)g.H[0] * s.n_img));
     s.rec_src = s.exp_rec.h;
     // host position of lane L's record i: exported, L * exp_lane + i; after a
@@ -1129,7 +1199,7 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
         s.n_final = host_finalize(p, s.h_ori.p, side_src, n_ori, s.keep.data(),
                                   s.img_count.data(), &s.fin_ws);
         // the next job in this slot exports this many records per lane
-        const unsigned lane_max = std::max(s.n_lane[0], s.n_lane[1]);
+        const unsigned lane_max = *std::max_element(s.n_lane, s.n_lane + kLanes);
         if (lane_max > s.exp_lane)
             grow_export(s, ((double)lane_max + lane_max / 2) * kLanes, (size_t)8192 * s.n_img * kLanes);
     }
@@ -1139,8 +1209,11 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     s.t_host[3] = ms(t_copy, t_fin);
     s.t_host[5] = blocked;
 
-    s.counts.extrema = (int64_t)s.lane_n[0][0] + s.lane_n[0][1];
-    s.counts.refined = (int64_t)s.lane_n[1][0] + s.lane_n[1][1];
+    s.counts.extrema = s.counts.refined = 0;
+    for (int L = 0; L < kLanes; ++L) {
+        s.counts.extrema += s.lane_n[0][L];
+        s.counts.refined += s.lane_n[1][L];
+    }
     s.counts.oriented = n_ori;
     s.counts.final_n = (int64_t)s.n_final;
     s.counts.octaves = g.octaves;
@@ -1380,6 +1453,11 @@ int sift_hip_create(int device, sift_ctx** out) {
         if (v >= 0 && v <= 40) ctx->batch_px_log2 = ctx->batch_px_log2_alone = v;
     }
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_FLOW")) ctx->flow = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_EXT_SEG")) ctx->ext_seg_max = std::max(4, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_EXT_WAVES")) ctx->ext_waves = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_FLOW_PX")) ctx->flow_max_px = (size_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_FLOW_WGS")) ctx->flow_wgs = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("SIFT_LDS_PX"))
         ctx->lds_max_px = ctx->lds_max_px_shared = (size_t)std::max(0, std::atoi(e));
     bool ok = prepare_kernel_attributes() == hipSuccess;
@@ -1426,6 +1504,7 @@ int sift_hip_destroy(sift_ctx* ctx) {
     for (Slot& s : ctx->slots) {
         s.in.release();
         s.in8.release();
+        s.flow_ctr.release();
         s.pyr.release();
         s.tmp.release();
         s.cand.release();

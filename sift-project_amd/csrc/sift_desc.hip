@@ -21,8 +21,19 @@
 #ifndef SIFT_DESC_PERM  // 1: lanes sharing a replica take samples 16 apart (sample_of_lane)
 #define SIFT_DESC_PERM 0
 #endif
-#ifndef SIFT_DESC_BSTRIDE  // doubles between consecutive bins of a replica (>= replicas)
-#define SIFT_DESC_BSTRIDE SIFT_DSPLIT_REPS
+// Doubles between consecutive bins of a replica (>= replicas). ds_add_f64
+// serves a wave in four 16-lane groups, one LDS cycle each, 16 double slots
+// (double index mod 16; tools/lds_atomic_probe.hip, r06_s2: consecutive
+// doubles 4.0 cycles per instruction, stride 2 or 8 lanes per address 8.0).
+// With 8 interleaved replicas (stride 8) the two lanes of a group that share
+// a replica collide whenever their bins have the same parity; stride 9 maps
+// bin i of replica r to slot 9i + r (mod 16), so they collide only for bins
+// equal mod 16. Stride 9 keeps 4 workgroups per CU (39 KB of LDS); 10 and 11
+// do not. Alone per 1080p image (r06_s5, two boxes): stride 8 133-154 us,
+// 9 120-123 us, 10 / 11 149-151 us; synchronous latency -4 %; the driver's
+// command +-0.6 %. Every histogram is bit-identical (hist_slot relocates).
+#ifndef SIFT_DESC_BSTRIDE
+#define SIFT_DESC_BSTRIDE 9
 #endif
 #ifndef SIFT_DESC_RMAJOR  // > 0: replica-major layout, replicas SIFT_DESC_RMAJOR + 128 doubles apart
 #define SIFT_DESC_RMAJOR 0

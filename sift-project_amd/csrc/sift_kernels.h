@@ -22,7 +22,7 @@ hipError_t prepare_kernel_attributes();
 hipError_t launch_u8_to_f64(const uint8_t* in, double* out, size_t n, hipStream_t s);
 // zero a job's counters and set its age rank in its device tables
 hipError_t launch_job_begin(PyrTable* pt, const JobPrio& jp, unsigned* ctr, int n_ctr,
-                            hipStream_t s);
+                            unsigned* ctr2, int n_ctr2, hipStream_t s);
 hipError_t launch_prepare(const double* in, size_t in_bs, int w, int h, int c, int dbl,
                           double* out, size_t out_bs, int W0, int H0, int n_img, hipStream_t s);
 // e0/e1: optional HIP events timestamped by the dispatch itself (profiling);
@@ -50,6 +50,12 @@ LdsShape lds_shape(int W_first, int H_first, bool has_next, int n_gauss);
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
                               const BlurTaps* d_taps, int n_img, int W_first, int H_first,
                               hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+// the levels of the octaves of `fg` (all images) in one launch of `wgs`
+// persistent workgroups; ctr: fg's counters, word 0 the task ticket, all
+// zero before the launch (k_job_begin)
+hipError_t launch_octaves_flow(const PyrTable* d_pt, const FlowGrid& fg, const BlurTaps* d_taps,
+                               unsigned* ctr, int wgs, hipStream_t s, hipEvent_t e0,
+                               hipEvent_t e1);
 // snap (optional): the last workgroup writes the lane counter snapshot
 // (candidate end, raw / record begins) for the keypoint chain; snap[3] must
 // be zero before the launch.

@@ -764,28 +764,42 @@ __global__ __launch_bounds__(256) void k_blur_pair_dma(const double* __restrict_
 // ---------------------------------------------------------------------------
 constexpr int kTileW = 64, kTileH = 32;
 
-template <int R, bool DECIM>
-__global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ src, size_t src_bs,
-                                                   double* __restrict__ dst, size_t bs, int W,
-                                                   int H, BlurTaps taps,
-                                                   double* __restrict__ dec, int Wd, int Hd) {
-    set_job_prio(taps.jp, SIFT_PRIO_TILE);
+// Plane access of a tile: plain, or (SC1, k_octaves_flow) sc1 loads and
+// stores — write-through stores and L1-bypassing loads, the hand-off form of
+// the flow kernel (MI355X_MICROARCH "Valid forms", row 1)
+template <bool SC1>
+__device__ __forceinline__ double tile_ld(const double* p) {
+    if (SC1) {
+        const unsigned long long b =
+            __hip_atomic_load((const __attribute__((address_space(1))) unsigned long long*)p,
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __longlong_as_double((long long)b);
+    }
+    return *gbl(p);
+}
+template <bool SC1>
+__device__ __forceinline__ void tile_st(double* p, double v) {
+    if (SC1)
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)p,
+                           (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
+// One 64 x 32 output tile (bx, by) of a level; sin_ holds (32+2R) x
+// ((64+2R) | 1) doubles of LDS. Every thread of the 256 takes part.
+template <int R, bool DECIM, bool SC1>
+__device__ __forceinline__ void blur_tile_body(const double* __restrict__ src,
+                                               double* __restrict__ dst, int W, int H,
+                                               const BlurTaps& taps, double* __restrict__ dec,
+                                               int Wd, int Hd, int bx, int by, double* sin_) {
     constexpr int SH = kTileH + 2 * R;             // staged rows
     constexpr int SWp = (kTileW + 2 * R) | 1;      // staged row stride (odd)
     constexpr int RX = 4, RY = 8;                  // output runs per task
-    // one LDS region: the staged source, overwritten in place by the row
-    // pass (results held in registers across a barrier), so a tile workgroup
-    // takes 23-35 KB instead of 44-62 KB and more of them (and of other jobs'
-    // kernels) fit on a CU
-    __shared__ double sin_[SH * SWp];
     double* const tmp = sin_;
     constexpr int TS = SWp;  // row-pass row stride (odd)
     const int tid = threadIdx.x;
-    int bx, by, bz;
-    xcd_remap(bx, by, bz);
-    gdouble* g = gbl(src + bz * src_bs);
-    dst += bz * bs;
-    if (DECIM) dec += bz * bs;
     const int x0 = bx * kTileW, y0 = by * kTileH;
     double k[R + 1];
 #pragma unroll
@@ -801,7 +815,7 @@ __global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ sr
             const int i = tid + 256 * it;
             const int r = i / (kTileW + 2 * R), c = i - r * (kTileW + 2 * R);
             const int gy = clampi(y0 - R + r, 0, H - 1), gx = clampi(x0 - R + c, 0, W - 1);
-            v[it] = (i < N) ? g[(size_t)gy * W + gx] : 0.0;
+            v[it] = (i < N) ? tile_ld<SC1>(src + (size_t)gy * W + gx) : 0.0;
         }
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
@@ -865,14 +879,187 @@ __global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ sr
             const int y = y0 + r0 + j;
             if (x < W && y < H) {
                 const double o = div_sum_w(acc[j], sw, inv);
-                dst[(size_t)y * W + x] = o;
+                tile_st<SC1>(dst + (size_t)y * W + x, o);
                 if (DECIM && !(x & 1) && !(y & 1) && (x >> 1) < Wd && (y >> 1) < Hd)
-                    dec[(size_t)(y >> 1) * Wd + (x >> 1)] = o;
+                    tile_st<SC1>(dec + (size_t)(y >> 1) * Wd + (x >> 1), o);
             }
         }
     }
 }
+
+template <int R, bool DECIM>
+__global__ __launch_bounds__(256) void k_blur_tile(const double* __restrict__ src, size_t src_bs,
+                                                   double* __restrict__ dst, size_t bs, int W,
+                                                   int H, BlurTaps taps,
+                                                   double* __restrict__ dec, int Wd, int Hd) {
+    set_job_prio(taps.jp, SIFT_PRIO_TILE);
+    // one LDS region: the staged source, overwritten in place by the row
+    // pass (results held in registers across a barrier), so a tile workgroup
+    // takes 23-35 KB instead of 44-62 KB and more of them (and of other jobs'
+    // kernels) fit on a CU
+    __shared__ double sin_[(kTileH + 2 * R) * ((kTileW + 2 * R) | 1)];
+    int bx, by, bz;
+    xcd_remap(bx, by, bz);
+    if (DECIM) dec += bz * bs;
+    blur_tile_body<R, DECIM, false>(src + bz * src_bs, dst + bz * bs, W, H, taps, dec, Wd, Hd, bx,
+                                    by, sin_);
+}
 static_assert(kTileH == 4 * 8, "column pass: 256 threads = 64 columns x 4 runs of 8 rows");
+
+// ---------------------------------------------------------------------------
+// k_octaves_flow: the levels of consecutive small octaves (1080p: octaves
+// 2/3-5) in ONE launch instead of one launch per level. Levels that small
+// are latency-bound (~5 us per dependent launch alone for a few hundred KB,
+// and, in a job alone, each launch waits for CU slots behind the keypoint
+// chains), so the launch boundaries, not the bytes, set their time.
+// Persistent workgroups take 64 x 32 tiles (blur_tile_body, the arithmetic
+// of k_blur_tile: bit-identical planes) from a ticket in topological order:
+// octave, level, band of 32 rows, image, tile. A tile of level l waits until
+// the bands it reads of level l-1 (its own band +-1: R <= 32) — or, for
+// level 1, the bands of the previous octave's level `intervals` whose even
+// rows the decimated plane holds — have all their tiles; a tile waits only
+// on tiles with smaller tickets, held by running workgroups, so the launch
+// cannot deadlock. Hand-off (MI355X_MICROARCH "Valid forms", row 1): every
+// plane value is stored and loaded sc1 (write-through / L1-bypassing); each
+// wave drains its stores (vmcnt 0), the workgroup's barrier, then one lane's
+// agent-scope add to the band counter; the consumer's one lane polls the
+// counters with sc1 loads, the workgroup's barrier, then the loads. Dynamic
+// LDS pads each workgroup above half a CU's LDS: one per CU, the measured
+// configuration of that form. Waits are bounded (ctr[fg.err] = 1: never
+// expected; the planes are then wrong, never a hang).
+// ---------------------------------------------------------------------------
+constexpr int kFlowLdsDoubles = (kTileH + 2 * kFlowMaxR) * ((kTileW + 2 * kFlowMaxR) | 1);
+#ifndef SIFT_FLOW_PAD_KB
+#define SIFT_FLOW_PAD_KB 48
+#endif
+constexpr size_t kFlowPadBytes = SIFT_FLOW_PAD_KB * 1024;  // static + pad > 80 KB: one workgroup per CU
+constexpr unsigned long long kFlowGiveUp = 5000000;  // s_memrealtime ticks (100 MHz): 50 ms
+
+// (not inlined: one body per radius with its own registers; inlined into
+// the kernel's radius switch they shared one allocation and spilled)
+#ifdef SIFT_FLOW_INLINE
+#define SIFT_FLOW_TILE_ATTR __forceinline__
+#else
+#define SIFT_FLOW_TILE_ATTR __attribute__((noinline))
+#endif
+template <int R>
+__device__ SIFT_FLOW_TILE_ATTR void flow_tile(const double* src, double* dst, int W, int H,
+                                          const BlurTaps& taps, double* dec, int Wd, int Hd,
+                                          int bx, int by, double* lds) {
+    if (dec)
+        blur_tile_body<R, true, true>(src, dst, W, H, taps, dec, Wd, Hd, bx, by, lds);
+    else
+        blur_tile_body<R, false, true>(src, dst, W, H, taps, nullptr, 0, 0, bx, by, lds);
+}
+
+__global__ __launch_bounds__(256) void k_octaves_flow(const PyrTable* __restrict__ pt, FlowGrid fg,
+                                                      const BlurTaps* __restrict__ taps,
+                                                      unsigned* __restrict__ ctr) {
+    set_job_prio(pt->jp, SIFT_PRIO_TILE);
+    __shared__ __attribute__((aligned(16))) double lds[kFlowLdsDoubles];
+    extern __shared__ double flow_pad[];  // occupancy only (never touched)
+    __shared__ int s_task;
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    // Lane 0's work sits in ONE block per task, at its end (publish, then
+    // the next ticket), followed by the barrier: with a lane-0 block at the
+    // loop head as well, the compiler merged the two across the back edge
+    // and the other lanes looped on the same task without a new ticket. The
+    // task index is made wave-uniform (readfirstlane), so the exit is a
+    // scalar branch.
+    if (threadIdx.x == 0) s_task = (int)atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    for (;;) {
+        const int t = __builtin_amdgcn_readfirstlane(s_task);
+        if (t >= fg.total) break;
+        int gi = 0;
+        while (gi + 1 < fg.n_groups && t >= fg.g[gi + 1].first) ++gi;
+        const FlowGroup& G = fg.g[gi];
+        const int r = t - G.first;
+        const int per_band = fg.n_img * G.nbx;
+        const int by = r / per_band, rem = r - by * per_band;
+        const int im = rem / G.nbx, bx = rem - im * G.nbx;
+        const BlurTaps& tp = taps[G.l];
+        const int R = tp.R;
+#ifdef SIFT_FLOW_DEBUG
+        if (threadIdx.x == 0)
+            printf("wg %d task %d group %d (o %d l %d) band %d img %d tile %d R %d dep %d\n",
+                   (int)blockIdx.x, t, gi, G.o, G.l, by, im, bx, R, G.dep);
+#endif
+        if (threadIdx.x == 0 && G.dep >= 0) {
+            const FlowGroup& D = fg.g[G.dep];
+            int lo, hi;
+            if (!G.dep_dec) {  // rows [32 by - R, 32 by + 32 + R) of a same-size plane
+                lo = max(by - 1, 0);
+                hi = min(by + 1, D.nby - 1);
+            } else {  // decimated rows d come from the producer's rows 2 d
+                const int d0 = max(kTileH * by - R, 0), d1 = min(kTileH * by + kTileH - 1 + R, G.H - 1);
+                lo = min(2 * d0 / kTileH, D.nby - 1);
+                hi = min(2 * d1 / kTileH, D.nby - 1);
+            }
+            const unsigned need = (unsigned)D.nbx;
+            const unsigned long long t_give_up = __builtin_amdgcn_s_memrealtime() + kFlowGiveUp;
+            for (int b2 = lo; b2 <= hi; ++b2) {
+                gu32* c = (gu32*)&ctr[D.cnt + im * D.nby + b2];
+                while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() > t_give_up) {  // flag it, go on
+                        __hip_atomic_store((gu32*)&ctr[fg.err], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const double* src = plane(pt, im, G.o, G.l - 1);
+        double* dst = pt->lvl[G.o][G.l] + (size_t)im * pt->img_stride;
+        double* dec = G.dec ? pt->lvl[G.o + 1][0] + (size_t)im * pt->img_stride : nullptr;
+        const int Wd = G.dec ? pt->w[G.o + 1] : 0, Hd = G.dec ? pt->h[G.o + 1] : 0;
+        switch (R) {
+#define SIFT_FLOW_R(RR)                                                            \
+    case RR:                                                                       \
+        flow_tile<RR>(src, dst, G.W, G.H, tp, dec, Wd, Hd, bx, by, lds);           \
+        break;
+            SIFT_FLOW_R(1) SIFT_FLOW_R(2) SIFT_FLOW_R(3) SIFT_FLOW_R(4) SIFT_FLOW_R(5)
+            SIFT_FLOW_R(6) SIFT_FLOW_R(7) SIFT_FLOW_R(8) SIFT_FLOW_R(9) SIFT_FLOW_R(10)
+            SIFT_FLOW_R(11) SIFT_FLOW_R(12)
+#undef SIFT_FLOW_R
+            default:
+                break;  // the host never builds such a group (kFlowMaxR)
+        }
+        // publish: this wave's sc1 stores have completed, every wave's
+        // (barrier), then one add for the workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add((gu32*)&ctr[G.cnt + im * G.nby + by], 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#ifdef SIFT_FLOW_DEBUG
+            printf("wg %d task %d done: ctr[%d] = %u\n", (int)blockIdx.x, t,
+                   G.cnt + im * G.nby + by, ctr[G.cnt + im * G.nby + by]);
+#endif
+            s_task = (int)atomicAdd(&ctr[0], 1u);
+        }
+        __syncthreads();
+    }
+    (void)flow_pad;
+}
+
+hipError_t launch_octaves_flow(const PyrTable* d_pt, const FlowGrid& fg, const BlurTaps* d_taps,
+                               unsigned* ctr, int wgs, hipStream_t s, hipEvent_t e0,
+                               hipEvent_t e1) {
+    static bool attr = false;  // (benign race: idempotent)
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&k_octaves_flow),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFlowPadBytes);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int n = std::max(1, std::min(wgs, fg.total));
+    return launch_timed(k_octaves_flow, dim3(n), dim3(256), kFlowPadBytes, s, e0, e1, d_pt, fg,
+                        d_taps, ctr);
+}
 
 // ---------------------------------------------------------------------------
 // k_octaves_lds: every remaining small octave (W*H <= kLdsOctavePx) in ONE
@@ -1971,14 +2158,17 @@ __global__ __launch_bounds__(256) void k_u8_to_f64(const uint8_t* __restrict__ i
 // small launch instead of a table upload (a copy kernel reading pinned host
 // memory, ~8 us) and a memset (~5 us) ahead of the first blur.
 __global__ __launch_bounds__(256) void k_job_begin(PyrTable* __restrict__ pt, JobPrio jp,
-                                                   unsigned* __restrict__ ctr, int n_ctr) {
+                                                   unsigned* __restrict__ ctr, int n_ctr,
+                                                   unsigned* __restrict__ ctr2, int n_ctr2) {
     for (int i = threadIdx.x; i < n_ctr; i += blockDim.x) ctr[i] = 0u;
+    for (int i = threadIdx.x; i < n_ctr2; i += blockDim.x) ctr2[i] = 0u;
     if (threadIdx.x == 0) pt->jp = jp;
 }
 
 hipError_t launch_job_begin(PyrTable* pt, const JobPrio& jp, unsigned* ctr, int n_ctr,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(k_job_begin, dim3(1), dim3(256), 0, s, pt, jp, ctr, n_ctr);
+                            unsigned* ctr2, int n_ctr2, hipStream_t s) {
+    hipLaunchKernelGGL(k_job_begin, dim3(1), dim3(256), 0, s, pt, jp, ctr, n_ctr, ctr2,
+                       ctr2 ? n_ctr2 : 0);
     return hipGetLastError();
 }
 

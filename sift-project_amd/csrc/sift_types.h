@@ -102,6 +102,26 @@ struct PyrTable {
     JobPrio jp;
 };
 
+// Octaves in flight (k_octaves_flow): the levels of consecutive small
+// octaves in ONE launch, 64 x 32 tiles as k_blur_tile, each tile started as
+// soon as the rows it reads exist. Group i = one (octave, level >= 1) of every
+// image: tasks [first, next group's first), ordered (band, image, tile);
+// band counters at ctr[cnt + image * nby + band] count its finished tiles.
+// dep: the group whose plane it reads (-1: written before the launch);
+// dep_dec: that plane is the decimated one (2x the rows).
+constexpr int kFlowMaxGroups = 48;
+constexpr int kFlowMaxR = 12;  // radii the flow kernel instantiates
+struct FlowGroup {
+    int o, l, W, H, nbx, nby;
+    int first, cnt;
+    int dep, dep_dec, dec;
+};
+struct FlowGrid {
+    int n_groups, total, n_img;
+    int err;  // ctr word set when a dependency wait gave up (never expected)
+    FlowGroup g[kFlowMaxGroups];
+};
+
 // Streaming extrema tasks: centre columns per wavefront strip (64 lanes
 // minus the two halo lanes); centre rows per task are chosen per octave.
 constexpr int kExtSpan = 62;

@@ -269,6 +269,47 @@ def test_gpu_pyramid_paths_match_oracle(lds_px, shape):
         ctx.close()
 
 
+# The small octaves in flight (k_octaves_flow) against the oracle, level by
+# level: the default split, every octave up to 4 Mpx in one launch with one
+# workgroup (every dependency met in ticket order), 7 and 128 workgroups
+# (tiles waiting on their neighbour bands, decimated planes across octaves),
+# and the per-level launches (SIFT_FLOW=0).
+@pytest.mark.parametrize("flow", [("1", "524288", "128"), ("1", "4194304", "1"),
+                                  ("1", "4194304", "7"), ("1", "4194304", "128"),
+                                  ("0", "0", "1")],
+                         ids=["default", "all-1wg", "all-7wg", "all-128wg", "off"])
+@pytest.mark.parametrize("shape", [(640, 360, 1), (333, 517, 3), (97, 61, 1)],
+                         ids=["640x360", "333x517rgb", "97x61"])
+def test_gpu_octaves_flow_match_oracle(flow, shape):
+    import os
+
+    from sift_hip import Context
+
+    env = {"SIFT_FLOW": flow[0], "SIFT_FLOW_PX": flow[1], "SIFT_FLOW_WGS": flow[2],
+           "SIFT_BATCH_PX_LOG2": "18"}
+    os.environ.update(env)
+    try:
+        ctx = Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    try:
+        w, h, c = shape
+        img = synth_image(w, h, c, seed=w * 5 + h)
+        ref = OracleRun(img)
+        for rep in range(2):  # the second job reuses the slot's counters
+            kps, df = ctx.detect(img, desc_f32=True)
+            for o in range(ref.octaves):
+                for lv in range(ref.levels):
+                    a, b = ctx.level(o, lv), ref.level(o, lv)
+                    assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (rep, o, lv)
+            assert np.array_equal(sort_extrema(ctx.extrema()), sort_extrema(ref.extrema))
+            r = compare_final(kps, df, ref.final, ref.desc_f32)
+            assert final_ok(r), r
+    finally:
+        ctx.close()
+
+
 # The descriptor (k_descriptor_split, every per-sample operation in f64)
 # against the 1080p golden and the stb-decoded photographs (natural
 # gradients).
