@@ -604,17 +604,23 @@ int enqueue_chain(sift_ctx* ctx, Slot& s, const ChainSpec& c) {
 // failed allocation falls back to the minimum, then to no buffer at all,
 // rather than failing the job (the hint is the context-wide largest
 // records-per-pixel seen, which one dense image can make large).
-constexpr size_t kExportMaxRecs = (size_t)1 << 22;  // both lanes: 704 MB + sides
+// Lanes split the buffer evenly among the lanes the job uses (s.lanes: one
+// for a pipelined job, kLanes for a job alone), so a pipelined job's single
+// lane gets all of it (sizing by kLanes doubled the pinned allocations and
+// their growth inside the timed jobs of config 5 when kLanes went to 4:
+// 9.97 -> 11.1 ms per image, r06_bigab).
+constexpr size_t kExportMaxRecs = (size_t)1 << 22;  // every lane: 704 MB + sides
 void grow_export(Slot& s, double want, size_t min_want) {
     const size_t w = (size_t)std::min<double>(want, (double)kExportMaxRecs);
     const size_t m = std::min(min_want, kExportMaxRecs);
+    const size_t lanes = (size_t)std::max(1, s.lanes);
     if (s.exp_rec.cap >= std::max(w, m) && s.exp_side.cap >= s.exp_rec.cap) {
-        s.exp_lane = s.exp_rec.cap / kLanes;
+        s.exp_lane = s.exp_rec.cap / lanes;
         return;
     }
     for (size_t n : {std::max(w, m), m}) {
         if (s.exp_rec.ensure(n) == SIFT_OK && s.exp_side.ensure(s.exp_rec.cap) == SIFT_OK) {
-            s.exp_lane = s.exp_rec.cap / kLanes;
+            s.exp_lane = s.exp_rec.cap / lanes;
             return;
         }
         s.exp_rec.release();
@@ -877,13 +883,13 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // the largest record count seen so far (a larger one falls back to one
     // bulk download at the end, and grows them for the next call)
     const double exp_hint =
-        ctx->exp_px_hint * 1.5 * (double)W0 * (double)H0 * n_img * kLanes;
-    grow_export(s, std::max<double>(exp_hint, (double)s.exp_rec.cap), (size_t)8192 * n_img * kLanes);
+        ctx->exp_px_hint * 1.5 * (double)W0 * (double)H0 * n_img * lanes;
+    grow_export(s, std::max<double>(exp_hint, (double)s.exp_rec.cap), (size_t)8192 * n_img * lanes);
     if ((st = s.exp_cnt.ensure(kExportCntWords * (kMaxOctaves + 2))) != SIFT_OK) return st;
     // poison: a range no launch published reads as "not exported"
     std::fill(s.exp_cnt.h, s.exp_cnt.h + s.exp_cnt.cap, 0xFFFFFFFFu);
     // lane L exports its records (lane-local index i) to exp_rec[L * exp_lane + i]
-    s.exp_lane = s.exp_rec.cap / kLanes;
+    // (exp_lane = cap / lanes, set by grow_export; 0: no buffer, bulk path)
 
     auto run_chain = [&](int L, int o_begin, int o_end, const unsigned* cand_begin,
                          unsigned* begin, hipStream_t sx) -> int {
@@ -1201,7 +1207,8 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
         // the next job in this slot exports this many records per lane
         const unsigned lane_max = *std::max_element(s.n_lane, s.n_lane + kLanes);
         if (lane_max > s.exp_lane)
-            grow_export(s, ((double)lane_max + lane_max / 2) * kLanes, (size_t)8192 * s.n_img * kLanes);
+            grow_export(s, ((double)lane_max + lane_max / 2) * s.lanes,
+                        (size_t)8192 * s.n_img * s.lanes);
     }
     const auto t_fin = clk::now();
     s.t_host[1] = ms(t0, t_wait);
