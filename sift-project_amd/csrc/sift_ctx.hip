@@ -310,6 +310,19 @@ struct sift_ctx {
     bool flow = false;
     size_t flow_max_px = (size_t)1 << 19;
     int flow_wgs = 128;
+    // octaves of at most fuse_max_px pixels (and above the LDS octaves): two
+    // k_octave_fused launches each (chain levels, tail levels) instead of one
+    // per level; tiles of 32 x 32 from fuse_t32_px pixels on, 16 x 16 below
+    // (SIFT_FUSE=1, SIFT_FUSE_PX, SIFT_FUSE_T32_PX). Bit-exact, off by
+    // default. Alone per 1080p image (r06_fuse2, r06_fuse3): octaves 4 / 5
+    // 20.5 / 20.4 us against 23.7 / 22.6 as per-level launches, the pyramid
+    // 395 vs 403 us (octave 2, 960 x 540, loses: 46.5 vs 27.6 us); but its
+    // 1024-thread, 58 KB workgroups hold CUs the concurrent keypoint chains
+    // need: synchronous latency 0.795 vs 0.763 ms, the driver's command
+    // 0.552 vs 0.542 ms per step, config 5 10.22 vs 9.67 ms per image.
+    bool fuse = false;
+    size_t fuse_max_px = (size_t)1 << 17;
+    size_t fuse_t32_px = 0;
     bool serial = false;  // SIFT_SERIAL=1: every kernel on one stream (profiling)
     // Kernels raise their waves' issue priority by their job's age rank
     // (JobPrio; -1.3 % on the driver's bench command, round 3); d_done
@@ -815,6 +828,30 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             o_flow = o_small;
         }
     }
+    // octaves [o_fuse, o_small): two k_octave_fused launches each (levels
+    // 1 .. intervals, the decimation chain, and the two tail levels; tiles
+    // with recomputed halos), from the first octave of at most fuse_max_px
+    // pixels whose tiles, and those of every smaller octave, fit in LDS
+    int o_fuse = o_small;
+    FusedOctave fchain[kMaxOctaves], ftail[kMaxOctaves];
+    if (ctx->fuse && o_flow == o_small) {
+        int radii[kMaxLevels] = {};
+        for (int l = 1; l < g.n_gauss; ++l) radii[l] = s.taps[l].R;
+        for (int o = o_small - 1; o >= 1; --o) {
+            const size_t px = (size_t)g.W[o] * g.H[o];
+            const int tile = px >= ctx->fuse_t32_px ? 32 : 16;
+            const int thr = tile >= 32 ? 1024 : 256;
+            const int Wd = o + 1 < g.octaves ? g.W[o + 1] : 0;
+            const int Hd = o + 1 < g.octaves ? g.H[o + 1] : 0;
+            if (px > ctx->fuse_max_px ||
+                !plan_octave_fused(o, g.n_gauss, 1, dec_level, g.W[o], g.H[o], Wd, Hd, radii, tile,
+                                   thr, &fchain[o]) ||
+                !plan_octave_fused(o, g.n_gauss, dec_level + 1, g.n_gauss - 1, g.W[o], g.H[o], Wd,
+                                   Hd, radii, tile, thr, &ftail[o]))
+                break;
+            o_fuse = o;
+        }
+    }
     SIFT_HIP_TRY(launch_job_begin(&s.d_stage->pt, s.h_pt.jp, s.d_ctr, kCtrWords,
                                   flow_words ? s.flow_ctr.p : nullptr, flow_words, sA));
 
@@ -966,7 +1003,26 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
             SIFT_HIP_TRY(launch_octaves_flow(d_pt, fg, s.d_stage->taps, s.flow_ctr.p,
                                              ctx->flow_wgs, sA, e0, e1));
         }
-        for (int l = 1; o < o_flow && l < g.n_gauss; ++l) {
+        if (o >= o_fuse) {  // the chain group on A, the tail group as the tail levels
+            for (const FusedOctave* fo : {&fchain[o], &ftail[o]}) {
+                const bool tail = fo == &ftail[o] && two_pyr && o < o_tail_end;
+                if (tail) {
+                    hipEvent_t chain_ev = sync_event(s);
+                    if (!chain_ev) return SIFT_ERR_HIP;
+                    SIFT_HIP_TRY(hipEventRecord(chain_ev, sA));
+                    SIFT_HIP_TRY(hipStreamWaitEvent(sB, chain_ev, 0));
+                }
+                double bytes =
+                    16.0 * (fo->l_last - fo->l_first + 1) * (double)g.W[o] * (double)g.H[o];
+                if (fo->dec_level >= 0) bytes += 8.0 * (double)fo->Wd * (double)fo->Hd;
+                hipEvent_t e0, e1;
+                if (prof_events(ctx, s, &e0, &e1, bytes * n_img, SIFT_PROF_PYRAMID + o) != SIFT_OK)
+                    return SIFT_ERR_HIP;
+                SIFT_HIP_TRY(launch_octave_fused(d_pt, *fo, s.d_stage->taps, n_img,
+                                                 tail ? sB : sA, e0, e1));
+            }
+        }
+        for (int l = 1; o < o_flow && o < o_fuse && l < g.n_gauss; ++l) {
             const bool tail = two_pyr && l > dec_level && o < o_tail_end;
             hipStream_t so = tail ? sB : sA;
             if (tail && l == dec_level + 1) {
@@ -1465,6 +1521,10 @@ int sift_hip_create(int device, sift_ctx** out) {
     if (const char* e = std::getenv("SIFT_EXT_WAVES")) ctx->ext_waves = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("SIFT_FLOW_PX")) ctx->flow_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_FLOW_WGS")) ctx->flow_wgs = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_FUSE")) ctx->fuse = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SIFT_FUSE_PX")) ctx->fuse_max_px = (size_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SIFT_FUSE_T32_PX"))
+        ctx->fuse_t32_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_LDS_PX"))
         ctx->lds_max_px = ctx->lds_max_px_shared = (size_t)std::max(0, std::atoi(e));
     bool ok = prepare_kernel_attributes() == hipSuccess;

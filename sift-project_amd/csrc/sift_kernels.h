@@ -50,6 +50,24 @@ LdsShape lds_shape(int W_first, int H_first, bool has_next, int n_gauss);
 hipError_t launch_octaves_lds(const PyrTable* d_pt, int o_first, int o_last, int n_gauss,
                               const BlurTaps* d_taps, int n_img, int W_first, int H_first,
                               hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+// levels [l_first, l_last] of one octave in one launch, tiled with
+// recomputed halos (k_octave_fused; the base is level l_first - 1);
+// plan_octave_fused returns false when a tile's regions do not fit in LDS or
+// a radius is outside 1..12. radii[l]: level l's taps.
+constexpr size_t kFusedMaxBytes = 160 * 1024;
+struct FusedOctave {
+    int o, n_gauss, W, H, Wd, Hd, dec_level;  // dec_level -1: no decimation in the group
+    int l_first, l_last;                      // levels of the launch
+    int tw, th, ntx, nty;                     // tile core, tiles across / down
+    int R[kMaxLevels];                        // radius of level l
+    int halo[kMaxLevels];                     // R[l+1] + ... + R[l_last]
+    int capS, capT, threads;                  // LDS doubles: level region, temporary
+    size_t bytes;                             // dynamic LDS of the launch
+};
+bool plan_octave_fused(int o, int n_gauss, int l_first, int l_last, int W, int H, int Wd, int Hd,
+                       const int* radii, int tile, int threads, FusedOctave* f);
+hipError_t launch_octave_fused(const PyrTable* d_pt, const FusedOctave& f, const BlurTaps* d_taps,
+                               int n_img, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // the levels of the octaves of `fg` (all images) in one launch of `wgs`
 // persistent workgroups; ctr: fg's counters, word 0 the task ticket, all
 // zero before the launch (k_job_begin)

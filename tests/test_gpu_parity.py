@@ -310,6 +310,55 @@ def test_gpu_octaves_flow_match_oracle(flow, shape):
         ctx.close()
 
 
+# Mid-sized octaves fused into one launch each (k_octave_fused: tiles with
+# recomputed halos) against the oracle, level by level: the default split,
+# every octave from octave 1 on with 32 x 32 or 16 x 16 tiles, without the
+# LDS-resident octaves (so tiny octaves, down to a few pixels, are tiled
+# too), other intervals (halos of 4 to 8 levels), and two jobs per context
+# (the second reuses the slot). Ragged shapes give partial tiles and tiles
+# whose halos are clipped on every side.
+@pytest.mark.parametrize("fuse", [
+    ({"SIFT_FUSE": "1"}, None),
+    ({"SIFT_FUSE": "1", "SIFT_FUSE_PX": "4194304", "SIFT_FUSE_T32_PX": "0"}, None),
+    ({"SIFT_FUSE": "1", "SIFT_FUSE_PX": "4194304", "SIFT_FUSE_T32_PX": "4194304",
+      "SIFT_LDS_PX": "0"}, None),
+    ({"SIFT_FUSE": "1", "SIFT_FUSE_PX": "4194304", "SIFT_LDS_PX": "0"}, {"intervals": 1}),
+    ({"SIFT_FUSE": "1", "SIFT_FUSE_PX": "4194304", "SIFT_FUSE_T32_PX": "0"},
+     {"intervals": 5, "init_sigma": 1.3}),
+], ids=["default", "all-t32", "all-t16-nolds", "int1-nolds", "int5-t32"])
+@pytest.mark.parametrize("shape", [(640, 360, 1), (333, 517, 3), (97, 61, 1)],
+                         ids=["640x360", "333x517rgb", "97x61"])
+def test_gpu_octave_fused_match_oracle(fuse, shape):
+    import os
+
+    from sift_hip import Context, SiftParams
+
+    env, kw = fuse
+    env = dict(env, SIFT_BATCH_PX_LOG2="18")
+    os.environ.update(env)
+    try:
+        ctx = Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    try:
+        w, h, c = shape
+        img = synth_image(w, h, c, seed=w * 3 + h)
+        p = SiftParams(**kw) if kw else None
+        ref = OracleRun(img, p)
+        for rep in range(2):
+            kps, df = ctx.detect(img, p, desc_f32=True)
+            for o in range(ref.octaves):
+                for lv in range(ref.levels):
+                    a, b = ctx.level(o, lv), ref.level(o, lv)
+                    assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (rep, o, lv)
+            assert np.array_equal(sort_extrema(ctx.extrema()), sort_extrema(ref.extrema))
+            r = compare_final(kps, df, ref.final, ref.desc_f32)
+            assert final_ok(r), r
+    finally:
+        ctx.close()
+
+
 # The descriptor (k_descriptor_split, every per-sample operation in f64)
 # against the 1080p golden and the stb-decoded photographs (natural
 # gradients).

@@ -42,11 +42,21 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=50)
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
+    ap.add_argument("--big", default="", help="a BASELINE config of bench.py (config3, config5)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
-    img = torch.from_numpy(synth_image(a.w, a.h, 1, seed=42)).cuda()
+    if a.big:
+        sys.path.insert(0, ROOT)
+        import bench  # noqa: E402  (BIG_CONFIGS)
+        spec = bench.BIG_CONFIGS[a.big]
+        a.w, a.h = spec["w"], spec["h"]
+        host = synth_image(a.w, a.h, 1, nblobs=spec["nblobs"], smax=spec["smax"], seed=42)
+        p = SiftParams(**spec["params"])
+    else:
+        host = synth_image(a.w, a.h, 1, seed=42)
+        p = SiftParams()
+    img = torch.from_numpy(host).cuda()
     torch.cuda.synchronize()
-    p = SiftParams()
     for v in a.variants:
         c = make(v, True)
         for _ in range(3):
