@@ -1,0 +1,20 @@
+#!/bin/bash
+# round 6: descriptor waves per record (SIFT_DESC_WAVES 4 / 2 / 1: more records in flight per CU) — parity, alone, A/B, config 5
+set -o pipefail
+R=$(pwd)
+O=$R/gpurun_out/r06_dw
+mkdir -p $O
+A=$R/sift-project_amd/alt
+L() { echo SIFT_HIP_LIB=$A/$1/libsift_hip.so; }
+timeout -k 10 400 python3 tools/kernel_alone.py --n 100 base $(L dw2) $(L dw1) base $(L dw2) $(L dw1) 2>&1 | grep -v amdgpu.ids | tee $O/alone.txt || exit 1
+for v in dw2 dw1; do
+  SIFT_HIP_LIB=$A/$v/libsift_hip.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "descriptor or big or golden or photo" > $O/pytest_$v.log 2>&1 || { tail -30 $O/pytest_$v.log; exit 1; }
+  echo "$v: $(tail -1 $O/pytest_$v.log)"
+done
+timeout -k 10 400 python3 tools/kernel_alone.py --big config5 --n 3 base $(L dw2) $(L dw1) 2>&1 | grep -v amdgpu.ids | tee $O/alone_c5.txt || exit 1
+bash tools/bench_ab.sh r06_dw/ab 3 base $(L dw2) $(L dw1) 2>&1 | tee $O/ab.txt
+for v in base dw2 dw1; do
+  lib=""; [ $v != base ] && lib=$A/$v/libsift_hip.so
+  SIFT_HIP_LIB=$lib timeout -k 10 200 python3 tools/big_profile.py config5 --images 12 > $O/c5_$v.json 2> $O/c5_$v.err || { tail -5 $O/c5_$v.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/c5_$v.json')); print('config5 $v', round(d['ms_per_image'],3))"
+done
