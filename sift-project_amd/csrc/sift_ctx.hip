@@ -371,6 +371,11 @@ struct sift_ctx {
     // and falls back to the bulk download + a full host sort: 12-17 ms on an
     // 8K image, the first two jobs of every config-5 leg in round 4)
     double exp_px_hint = 0.0;
+    // all records of a job per octave-0 pixel, the largest seen: a one-lane
+    // (pipelined) job puts every record in its lane, so its buffers are sized
+    // from this (sized from the lane hint, a job alone's largest lane, they
+    // overflowed into the bulk path on each slot's first pipelined job)
+    double exp_px_total = 0.0;
     Slot slots[kSlots];
     // two stream pairs, one per hardware queue each (HIP's default is four
     // queues per process): pair k = pyramid (high priority) + keypoint chains
@@ -920,7 +925,8 @@ int enqueue_job(sift_ctx* ctx, Slot& s, const void* const* images, int kind) {
     // the largest record count seen so far (a larger one falls back to one
     // bulk download at the end, and grows them for the next call)
     const double exp_hint =
-        ctx->exp_px_hint * 1.5 * (double)W0 * (double)H0 * n_img * lanes;
+        (lanes == 1 ? ctx->exp_px_total : ctx->exp_px_hint * lanes) * 1.5 * (double)W0 *
+        (double)H0 * n_img;
     grow_export(s, std::max<double>(exp_hint, (double)s.exp_rec.cap), (size_t)8192 * n_img * lanes);
     if ((st = s.exp_cnt.ensure(kExportCntWords * (kMaxOctaves + 2))) != SIFT_OK) return st;
     // poison: a range no launch published reads as "not exported"
@@ -1202,6 +1208,8 @@ int finalize_job(sift_ctx* ctx, Slot& s) {
     ctx->exp_px_hint = std::max(ctx->exp_px_hint,
                                 (double)*std::max_element(s.n_lane, s.n_lane + kLanes) /
                                     ((double)g.W[0] * (double)g.H[0] * s.n_img));
+    ctx->exp_px_total =
+        std::max(ctx->exp_px_total, (double)n_ori / ((double)g.W[0] * (double)g.H[0] * s.n_img));
     s.rec_src = s.exp_rec.h;
     // host position of lane L's record i: exported, L * exp_lane + i; after a
     // bulk download, the lanes are concatenated
