@@ -359,6 +359,33 @@ def test_gpu_octave_fused_match_oracle(fuse, shape):
         ctx.close()
 
 
+# The fused initial blur of a one-channel input (gray + bilinear x2 through
+# the strip walk's ring of input rows, k_blur<R, 2, false, kSrcUpsample>) and
+# the octave-0 pair walk on doubled planes of >= 4 Mpx, against the oracle:
+# ragged strip and band counts (H0 not a multiple of the 32-row strips or the
+# 64-row pair bands), both image borders, and a wider initial kernel
+# (init_sigma 2.0: R = 5 instead of 4). (Round 6 measured the initial blur on
+# the pair walk too, with the ring walking up or down: bit-exact here, but
+# 63 vs 34 us per 1080p image, so it was removed.)
+@pytest.mark.parametrize("case", [((1100, 1001), {}), ((1030, 1027), {"init_sigma": 2.0})],
+                         ids=["1100x1001", "1030x1027-sigma2"])
+def test_gpu_initial_blur_large_match_oracle(gpu_ctx, case):
+    from sift_hip import SiftParams
+
+    (w, h), kw = case
+    img = synth_image(w, h, 1, seed=w + 7 * h)
+    p = SiftParams(**kw) if kw else None
+    ref = OracleRun(img, p)
+    kps, df = gpu_ctx.detect(img, p, desc_f32=True)
+    for o in range(2):
+        for lv in range(ref.levels):
+            a, b = gpu_ctx.level(o, lv), ref.level(o, lv)
+            assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (o, lv)
+    assert np.array_equal(sort_extrema(gpu_ctx.extrema()), sort_extrema(ref.extrema))
+    r = compare_final(kps, df, ref.final, ref.desc_f32)
+    assert final_ok(r), r
+
+
 # The descriptor (k_descriptor_split, every per-sample operation in f64)
 # against the 1080p golden and the stb-decoded photographs (natural
 # gradients).
