@@ -38,9 +38,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # stream each), two 8-image jobs (a stream pair each)
 JOB_DEPTH = max(1, min(8, int(os.environ.get("SIFT_JOB_DEPTH", "4"))))
 BATCH_DEPTH = max(1, min(8, int(os.environ.get("SIFT_BATCH_DEPTH", "2"))))
-# BASELINE configs 3 / 5: one large image per job, jobs in flight (3: config 3
-# 4.15 vs 4.36 ms per image at 2, config 5 10.5 vs 11.6 ms, round 5)
-BIG_DEPTH = max(1, min(8, int(os.environ.get("SIFT_BIG_DEPTH", "3"))))
+# BASELINE configs 3 / 5: one large image per job, jobs in flight (round 5:
+# 3 against 2, config 3 4.15 vs 4.36 ms per image, config 5 10.5 vs 11.6 ms;
+# round 6: 4 against 3, config 3 3.65 vs 3.71, config 5 9.40 vs 9.60,
+# gpurun_out/r06_depth; the 1080p legs stay at 4 single-image jobs: 3 / 5 / 6
+# in flight +6 / +10 / +14 % on the driver's command)
+BIG_DEPTH = max(1, min(8, int(os.environ.get("SIFT_BIG_DEPTH", "4"))))
 sys.path.insert(0, os.path.join(ROOT, "sift-project_amd"))
 
 import numpy as np  # noqa: E402
