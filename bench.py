@@ -905,7 +905,17 @@ def main() -> int:
         if world == 1 and not args.no_extra:
             out.update(extra_legs(ctx, dev, host_imgs, dev_imgs, W, H, params,
                                   args.extra_seconds))
+        if world == 1 and not args.no_matcher:
+            kps_a, _ = ctx.detect_device(dev_imgs[0].data_ptr(), W, H, 1, params)
+            out["matcher"] = matcher_bench(ctx, dev, kps_a, W, H, params,
+                                           0.0 if args.no_cpu_baseline else args.cpu_seconds)
         if world == 1 and not args.no_big:
+            # the 1080p context (its streams and their hardware queues, its
+            # slots' arenas) is released first: the big legs' jobs get the
+            # process's four hardware queues to themselves
+            if not use_exchange:
+                ctx.close()
+                ctx = None
             for name in ("config3", "config5"):
                 out[name] = big_config_leg(name, dev)
         if world == 1 and not args.no_cpu_baseline:
@@ -913,10 +923,6 @@ def main() -> int:
             ref = cpu_baseline_reference(host_imgs[0], args.cpu_seconds)
             if ref is not None:
                 out["cpu_baseline_reference"] = ref
-        if world == 1 and not args.no_matcher:
-            kps_a, _ = ctx.detect_device(dev_imgs[0].data_ptr(), W, H, 1, params)
-            out["matcher"] = matcher_bench(ctx, dev, kps_a, W, H, params,
-                                           0.0 if args.no_cpu_baseline else args.cpu_seconds)
         # the headline figures again, last, so a tail of the line carries them
         summ = {"keypoints_per_s": out["value"], "ms_per_step": out["ms_per_step"],
                 "pyramid_frac_chip": roofline["frac"],
@@ -940,7 +946,8 @@ def main() -> int:
         out["summary"] = summ
         print(json.dumps(out), file=json_out, flush=True)
 
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if use_exchange:
         dist.destroy_process_group()
     return 0
