@@ -71,13 +71,14 @@
 // SIFT_BLUR_DMA_MAXR. Measured (tools/blur_lab.hip, r06_s1 / r06_s2, every
 // plane bit-identical): 4096^2 R = 5 / 7 / 10 -4.8 / -13.8 / -3.8 %, 8192^2
 // R = 5 / 7 -5.6 / -11.1 % but R = 10 +5.4 %, 15360x8640 R = 4..8 -3.6..-5.3 %
-// but R = 10 +2.9 %, 3840x2160 (1080p's octave 0) +2.7..+6 %; ring depth 2 or
-// 8 no better than 4. In the pipelined big-config legs the kernel's larger
-// LDS footprint (52 KB per workgroup at R = 8) costs more than it saves:
-// config 5 10.01 vs 9.66 ms per image, config 3 3.63 vs 3.65 (r06_s3), so the
-// default is off; the kernel stays as the measured alternative.
+// but R = 10 +2.9 %, 3840x2160 (1080p's octave 0) +2.7..+6 % (below the
+// 2^24-pixel threshold, so 1080p keeps k_blur_pair); ring depth 2 or 8 no
+// better than 4. In the pipelined big-config legs (4 jobs in flight, r06_dma2)
+// config 5 9.17 / 8.99 vs 9.42 / 9.29 ms per image, config 3 +-0.3 %;
+// pyramid alone at 8K -1.6 %, at 4096^2 -4 %. (An earlier A/B, r06_s3, had it
+// losing config 5, 10.01 vs 9.66, while the export buffers were mis-sized.)
 #ifndef SIFT_BLUR_DMA
-#define SIFT_BLUR_DMA 0
+#define SIFT_BLUR_DMA 4
 #endif
 #ifndef SIFT_BLUR_DMA_MAXR
 #define SIFT_BLUR_DMA_MAXR 8
