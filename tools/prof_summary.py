@@ -29,7 +29,8 @@ def main(path, n_images=None):
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"{k[:40]:40s} {cnt[k]:6d} {v:10.1f} {v / cnt[k]:9.2f} {v / n_img:9.1f}")
     # kernel families as bench.py's roofline / keypoint_kernels_alone rows
-    fams = {"pyramid": ("k_blur", "k_blur_pair", "k_blur_tile", "k_octaves_lds"), "extrema": ("k_extrema",),
+    fams = {"pyramid": ("k_blur", "k_blur_pair", "k_blur_pair_dma", "k_blur_tile", "k_octaves_lds",
+                        "k_octaves_flow", "k_octave_fused"), "extrema": ("k_extrema",),
             "refine": ("k_refine",), "orientation": ("k_orient",), "descriptor": ("k_descriptor",)}
     print(f"\n{'family':12s} {'launches':>9s} {'us/image':>9s} {'avg us/launch':>14s}")
     for f, pre in fams.items():
