@@ -2,7 +2,7 @@
 # round 6: the driver's command three times on one box (the big legs now run with the 1080p context closed)
 set -o pipefail
 R=$(pwd)
-O=gpurun_out/r06_final3
+O=gpurun_out/${OUT:-r06_final3}
 mkdir -p $O
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
