@@ -1525,8 +1525,6 @@ int sift_hip_create(int device, sift_ctx** out) {
     }
     if (const char* e = std::getenv("SIFT_SERIAL")) ctx->serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("SIFT_FLOW")) ctx->flow = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SIFT_EXT_SEG")) ctx->ext_seg_max = std::max(4, std::atoi(e));
-    if (const char* e = std::getenv("SIFT_EXT_WAVES")) ctx->ext_waves = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("SIFT_FLOW_PX")) ctx->flow_max_px = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SIFT_FLOW_WGS")) ctx->flow_wgs = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("SIFT_FUSE")) ctx->fuse = std::atoi(e) != 0;
